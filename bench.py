@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the MI355X path tracer on the Book-2 final scene.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+it is launched under torch.distributed.run, one rank per GPU.  A *step* is one
+pass of the hot path over one batch: every pixel of the 1920x1080 scene-8 image
+advanced by F progressive frames (F samples per pixel), through rt_render.
+With N ranks the image rows are split into interleaved stripes and each step
+advances F*N frames, so every rank does a fixed 1920x1080xF samples per step
+(weak scaling).  value = all ranks' samples / max-over-ranks wall time of the
+K timed steps.  Inputs (scene buffers, image) are resident in HBM before the
+timed region.  The rank-0 JSON line carries the HIP-event kernel roofline and
+the CPU-oracle baseline (on a bounded sample).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "raytracing-book_amd"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=8)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--scene", type=int, default=8)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--frames-per-step", type=int, default=64, help="spp per step per rank")
+    p.add_argument("--depth", type=int, default=5)
+    p.add_argument("--spp-total", type=int, default=4096, help="sqrt_spp uniform (BASELINE C3: 4096)")
+    p.add_argument("--stripe-rows", type=int, default=16)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--png", default=None)
+    return p.parse_args()
+
+
+def cpu_baseline(scene, args):
+    """CPU oracle (oracle/, the build's scalar restatement; the reference has no
+    CPU path) timed on the host: full-width rows of the same image (1 stripe in
+    8), frames scaled to ~cpu_seconds.  Also returns the oracle's logical
+    record-traffic count (bytes/sample) on a small sample of the same config."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    import rtamd
+    threads = min(16, os.cpu_count() or 1)
+    osc = pyoracle.OracleScene(scene, max_depth=args.depth, spp=args.spp_total)
+    W, H = scene.width, scene.height
+    world_s = 8
+    rows = rtamd.local_rows(H, 0, world_s, args.stripe_rows)
+    # counted pass (bytes per sample), 1 frame
+    _, cnt = pyoracle.render(osc, rtamd.frame_rand_factors(args.seed, 0, 1), rank=0, world=world_s * 4,
+                             stripe_rows=args.stripe_rows, nthreads=threads, counters=True)
+    keys = ["framebuffer_bytes", "node_bytes", "prim_bytes", "material_bytes", "texel_bytes", "light_bytes"]
+    bytes_per_sample = sum(cnt[k] for k in keys) / max(1, cnt["samples"])
+    # timing pass
+    t = time.perf_counter()
+    pyoracle.render(osc, rtamd.frame_rand_factors(args.seed, 0, 1), rank=0, world=world_s,
+                    stripe_rows=args.stripe_rows, nthreads=threads)
+    t1 = time.perf_counter() - t
+    nf = max(1, min(64, int(args.cpu_seconds / max(t1, 1e-3))))
+    t = time.perf_counter()
+    pyoracle.render(osc, rtamd.frame_rand_factors(args.seed, 1, nf), first_frame=2, rank=0, world=world_s,
+                    stripe_rows=args.stripe_rows, nthreads=threads)
+    dt = time.perf_counter() - t
+    samples = W * rows * nf
+    return {
+        "value": samples / dt / 1e6,
+        "unit": "Msamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"scene {args.scene} {W}x{H}, rows of stripe 0/{world_s} ({rows} rows), {nf} frames "
+                  f"(= {samples} samples, {dt:.1f} s), depth {args.depth}",
+    }, bytes_per_sample, cnt
+
+
+def main():
+    args = parse()
+    import torch
+    import rtamd
+    from rtamd import dist as rdist
+
+    rank, world, local_rank = rdist.init_from_env()
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dev = local_rank
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.Stream(device=dev)
+
+    scene = rtamd.Scene(args.scene, args.width, args.height, seed=args.seed)
+    ctx = rtamd.RenderContext(devices=(dev,), rank=rank, world=world, stripe_rows=args.stripe_rows)
+    ctx.upload_scene(scene)
+    ctx.set_params(max_depth=args.depth, spp=args.spp_total)
+    ctx.resize(args.width, args.height)
+    padded = ctx.padded_rows
+    image = torch.zeros((padded, args.width, 4), dtype=torch.float32, device=f"cuda:{dev}")
+    ctx.bind_device_image(image.data_ptr(), image.numel() * 4)
+    ctx.set_stream(stream.cuda_stream)
+
+    F = args.frames_per_step * world          # frames per step (weak scaling: fixed samples per rank)
+    n_local_px = ctx.local_rows * args.width
+    total_steps = args.warmup + args.steps
+    factors = rtamd.frame_rand_factors(args.seed, 0, F * total_steps)
+    frame = 1
+
+    def step():
+        nonlocal frame
+        ctx.render(frame, factors[frame - 1:frame - 1 + F])
+        frame += F
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        ev = []
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            step()
+            e1.record(stream)
+            ev.append((e0, e1))
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    launches_per_step = math.ceil(F / 256)
+    t_max = elapsed
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        t_max = float(t.item())
+
+    samples_total = args.width * args.height * F * args.steps   # all ranks together
+    value = samples_total / t_max / 1e6
+
+    # RCCL gather of the accumulated stripes (reported separately, not in value)
+    torch.cuda.synchronize()
+    tg = time.perf_counter()
+    full = rdist.gather_image(image, args.height, world, args.stripe_rows)
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - tg) * 1e3
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.barrier()
+            torch.distributed.destroy_process_group()
+        return
+
+    if args.png:
+        rtamd.save_png(full, args.png)
+    nan_px = int(np.isnan(full[..., :3]).any(axis=-1).sum())
+
+    cpu = None
+    bps = None
+    if not args.no_cpu_baseline:
+        try:
+            cpu, bps, _ = cpu_baseline(scene, args)
+        except Exception as e:  # the baseline is reported, not required
+            log("cpu baseline failed:", repr(e))
+    if bps is None:
+        try:
+            with open(os.path.join(REPO, "bench", "bytes_per_sample.json")) as f:
+                bps = json.load(f)[f"scene{args.scene}_depth{args.depth}"]["bytes_per_sample"]
+        except Exception:
+            bps = None
+
+    avg_launch_ms = float(np.mean(kernel_ms)) / launches_per_step
+    samples_per_launch = n_local_px * min(F, 256)
+    roofline = None
+    if bps is not None:
+        achieved = bps * samples_per_launch / (avg_launch_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(os.path.join(REPO, "profiles", "traffic.json")) as f:
+                tj = json.load(f)
+            key = f"scene{args.scene}_{args.width}x{args.height}_f{min(F, 256)}_d{args.depth}"
+            traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "bytes_per_sample": round(bps, 1), "kernel": "render_kernel",
+                    "avg_launch_ms": round(avg_launch_ms, 3), "samples_per_launch": samples_per_launch}
+
+    out = {
+        "metric": "Msamples/sec (W×H×spp/s) on Book-2 final scene @1080p",
+        "value": round(value, 2),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic: seeded scene {args.scene} (seed={args.seed}), built in-process",
+        "config": {"workload": f"scene{args.scene} Book-2 final, {args.width}x{args.height}, "
+                               f"{args.frames_per_step} spp/step/rank, max_depth {args.depth}",
+                   "scene": args.scene, "width": args.width, "height": args.height,
+                   "spp_per_step": F, "max_depth": args.depth, "stripe_rows": args.stripe_rows,
+                   "parallelism": f"row-stripes x{world}"},
+        "gather_ms": round(gather_ms, 3),
+        "nan_pixels": nan_px,
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,133 @@
+/*
+ * rt.h — drop-in C ABI of the MI355X path tracer (librtamd.so).
+ *
+ * It replaces the OpenGL binding contract that the reference's Java host drives
+ * (SURVEY §8b).  Each entry point names the reference call it stands in for.
+ * All calls return 0 (RT_OK) or a negative RT_ERR_* code; the message of the
+ * last failure on a context is available from rt_last_error().  A context is
+ * used by one host thread at a time (the reference's GL-context rule); callers
+ * own every host buffer they pass (the library copies what it keeps).
+ */
+#ifndef RT_H
+#define RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rt_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = -1,  /* bad pointer/size/enum, record size mismatch       */
+    RT_ERR_DEVICE = -2,       /* HIP runtime failure                               */
+    RT_ERR_STATE = -3,        /* call order (e.g. render before resize)            */
+    RT_ERR_LIMIT = -4,        /* an implicit reference limit exceeded (SURVEY App.C)*/
+    RT_ERR_NOMEM = -5
+};
+
+/* SSBO binding points (compute.glsl:127-153, RaytraceModel.java:81-113) */
+enum {
+    RT_BIND_SPHERES = 0, RT_BIND_BVH = 1, RT_BIND_QUADS = 2,
+    RT_BIND_MEDIA = 3, RT_BIND_BOXES = 4, RT_BIND_LIGHTS = 5
+};
+
+
+#define RT_MAX_TEXTURES 8        /* uniform sampler2D textures[8], compute.glsl:23 */
+#define RT_MAX_RECORDS 65535     /* 16-bit indices in packed ids (App. C)          */
+#define RT_MAX_BVH_DEPTH 64      /* int stack[64], compute.glsl:229                */
+
+typedef struct rt_ctx rt_ctx;
+
+/* Create a context rendering on n_devices HIP devices (device_ids may be NULL
+ * for 0..n-1).  Rows are split in interleaved stripes over the devices; the
+ * result equals a 1-device render bit for bit.
+ * Replaces: Window.initGLFW/initShaderPrograms (Window.java:90-193). */
+int rt_create(int n_devices, const int* device_ids, rt_ctx** out);
+int rt_destroy(rt_ctx* ctx);
+const char* rt_last_error(rt_ctx* ctx);
+int rt_abi_version(void);
+
+/* Upload one SSBO's exact std430 bytes (rt_types.h records; lights = int count
+ * followed by count packed ints).  nbytes must be a multiple of the record size.
+ * Replaces: RaytraceModel.put{Spheres,BVHNodes,Quads,ConstantMediums,Boxes,
+ * Lights}ToProgram -> BufferObject.uploadData (RaytraceModel.java:138-246). */
+int rt_upload_buffer(rt_ctx* ctx, int binding, const void* bytes, size_t nbytes);
+
+/* Upload texture slot 0..7; rows tightly packed, row 0 first (glTexImage2D).
+ * Sampling follows GL_LINEAR + CLAMP_TO_EDGE (Texture.java:74-77).
+ * Replaces: Texture.putData (Texture.java:122-133). */
+int rt_upload_texture(rt_ctx* ctx, int slot, int format, int w, int h, const void* texels);
+
+/* The 28-float std140 camera block (rt_camera_ubo).
+ * Replaces: Camera.putToShaderProgram UBO upload (Camera.java:121-139). */
+int rt_set_camera(rt_ctx* ctx, const float ubo[28]);
+
+/* Uniforms max_depth, background, sqrt_spp, recip_sqrt_spp.
+ * Replaces: GuiRenderer.maxDepthUpdate, Camera.putToShaderProgram("background"),
+ * RaytraceExecutor.setSamplePerPixel (RaytraceExecutor.java:50-56). */
+int rt_set_params(rt_ctx* ctx, int max_depth, const float background[3],
+                  float sqrt_spp, float recip_sqrt_spp);
+
+/* (Re)allocate the RGBA32F accumulation image, zero-filled.
+ * Replaces: Texture.resize on the framebuffer callback (Window.java:116-129). */
+int rt_resize(rt_ctx* ctx, int w, int h);
+
+/* Run n_frames progressive frames.  Equal to n_frames x { frame_count =
+ * first_frame+i; u_rand_factor = rand_factors[i]; glDispatchCompute;
+ * glMemoryBarrier }.  Asynchronous on the context's stream(s).
+ * Replaces: RaytraceExecutor.raytrace (RaytraceExecutor.java:100-142). */
+int rt_render(rt_ctx* ctx, int first_frame, int n_frames, const float* rand_factors);
+
+/* Wait for all queued renders. */
+int rt_sync(rt_ctx* ctx);
+
+/* Copy the accumulation image (W*H*4 floats, row 0 = top) to the host.
+ * Replaces: glGetTexImage in Texture.saveAsPNG (Texture.java:93). */
+int rt_read_image(rt_ctx* ctx, float* rgba);
+
+/* Overwrite the accumulation image (resume a checkpointed accumulation). */
+int rt_write_image(rt_ctx* ctx, const float* rgba);
+
+/* Device time of the last rt_render call (max over devices), after completion.
+ * Replaces: QueryTimer GL_TIME_ELAPSED (QueryTimer.java:24-50). */
+int rt_last_render_ns(rt_ctx* ctx, uint64_t* ns);
+
+/* ---- MI355X-native extensions (no reference counterpart) ---------------- */
+
+/* Multi-process partition (one process per GPU): this context renders only the
+ * rows r with (r / stripe_rows) % world == rank.  Its image then holds
+ * local_rows = rt_local_rows(...) rows, stripe-compacted; gather with
+ * torch.distributed (RCCL) and rt_deinterleave_rows().  Must precede rt_resize. */
+int rt_set_partition(rt_ctx* ctx, int rank, int world, int stripe_rows);
+int rt_local_rows(int height, int rank, int world, int stripe_rows);
+int rt_padded_local_rows(int height, int world, int stripe_rows);
+
+/* Bind a caller-owned device buffer (>= W*local_rows*16 bytes, on the context's
+ * single device) as the accumulation image instead of an internal one; pass
+ * NULL to go back to the internal image.  Must follow rt_resize. */
+int rt_bind_device_image(rt_ctx* ctx, void* device_ptr, size_t nbytes);
+
+/* Use a caller-provided hipStream_t (e.g. torch's current stream); NULL = own. */
+int rt_set_stream(rt_ctx* ctx, void* hip_stream);
+
+/* Host helper: scatter gathered stripe blocks [world][padded_rows][W][4] into a
+ * full W x H image (row 0 = top). */
+int rt_deinterleave_rows(const float* gathered, int width, int height, int world,
+                         int stripe_rows, float* rgba_out);
+
+/* Per-frame u_rand_factor for frame index f (0-based) of a seeded render:
+ * top 24 bits of splitmix64(seed, f) / 2^24, in [0,1).  Stands in for the
+ * reference's (float)Math.random() per frame (RaytraceExecutor.java:124). */
+float rt_frame_rand_factor(uint64_t seed, uint64_t frame_index);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_H */

@@ -1,0 +1,29 @@
+/*
+ * rt_debug.h — test/diagnostic hooks exported by librtamd.so (not part of the
+ * reference's interface; used by tests/ to check device-side pieces directly).
+ */
+#ifndef RT_DEBUG_H
+#define RT_DEBUG_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Evaluate a GLSL built-in of rt_glsl.h on `device` (fn: 0 sin, 1 cos, 2 log,
+ * 3 acos, 4 atan2(x, y), 5 fract, 6 sqrt). */
+int rt_debug_eval_builtin(int device, int fn, const float* x, const float* y, float* out, int n);
+
+/* Host-only: the threaded-BVH re-layout rt_upload_buffer(RT_BIND_BVH) builds
+ * (32-byte rt_dnode records); out may be NULL to query the count. */
+int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t out_cap, int* n_out);
+
+/* Number of visible HIP devices (0 when none). */
+int rt_debug_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,218 @@
+/*
+ * rt_glsl.h — the GLSL 4.30 built-in functions the reference shader relies on,
+ * defined once, deterministically, for both sides of the parity check.
+ *
+ * In the reference the built-ins (sin, cos, log, acos, atan, pow, sqrt,
+ * normalize, reflect, refract, mix, fract, mod, dot, cross, texture2D ...) are
+ * implemented by the GPU vendor's GLSL compiler (SURVEY §8c "Third-party
+ * arithmetic"), so their bits are unpinned.  This header *is* our definition of
+ * them.  Every function uses only IEEE-754 binary32 +,-,*,/, sqrt, fma, floor,
+ * rint and exact integer/bit operations, so the same source compiled by g++
+ * (oracle, x86-64 SSE) and by hipcc (gfx950 kernel) produces identical bits as
+ * long as both are built with -ffp-contract=off and without fast-math
+ * (correctly-rounded f32 div/sqrt is hipcc's default).  tests/test_glsl_math.py
+ * pins each transcendental against libm in double precision (ulp bounds).
+ *
+ * Shared by: oracle/rt_oracle.cpp (CPU restatement, test infrastructure) and
+ * raytracing-book_amd/csrc/rt_kernel.hip (the product).  Nothing above the
+ * built-in level (traversal, shading, sampling) lives here.
+ */
+#ifndef RT_GLSL_H
+#define RT_GLSL_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RT_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#include <string.h>
+#define RT_HD static inline
+#endif
+
+/* compute.glsl:7 — "INFINITY" is FLT_MAX-ish, not IEEE inf. */
+#define RT_INFINITY 3.402823E+38f
+/* math.glsl:1 — const float PI = 3.14159265359 (rounds to 0x40490fdb). */
+#define RT_PI 3.14159265359f
+
+/* ---------------------------------------------------------------- bits */
+RT_HD uint32_t rt_f2u(float f) {
+#if defined(__HIPCC__)
+    return __float_as_uint(f);
+#else
+    uint32_t u; memcpy(&u, &f, 4); return u;
+#endif
+}
+RT_HD float rt_u2f(uint32_t u) {
+#if defined(__HIPCC__)
+    return __uint_as_float(u);
+#else
+    float f; memcpy(&f, &u, 4); return f;
+#endif
+}
+RT_HD int rt_isnan(float x) { return x != x; }
+
+/* float -> int with C truncation; NaN -> 0, saturating outside int range.
+ * (GLSL leaves out-of-range conversion undefined; this is our definition.) */
+RT_HD int rt_f2i(float x) {
+    if (!(x == x)) return 0;
+    if (x >= 2147483520.0f) return 2147483647;
+    if (x <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)x;
+}
+
+/* GLSL 4.30 §8.3: min(x,y) = y < x ? y : x ; max(x,y) = x < y ? y : x */
+RT_HD float g_min(float x, float y) { return (y < x) ? y : x; }
+RT_HD float g_max(float x, float y) { return (x < y) ? y : x; }
+RT_HD float g_fract(float x) { return x - floorf(x); }
+/* GLSL mod(x,y) = x - y*floor(x/y) */
+RT_HD float g_mod(float x, float y) { return x - y * floorf(x / y); }
+/* GLSL normalize() applied to a scalar (pdf.glsl:33): x/|x| = sign, NaN at 0 */
+RT_HD float g_normalize1(float x) { return x / fabsf(x); }
+
+/* ---------------------------------------------------------------- vec */
+struct v3 { float x, y, z; };
+struct v2 { float x, y; };
+
+RT_HD v3 mk3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+RT_HD v3 mk3s(float s) { return mk3(s, s, s); }
+RT_HD v3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+RT_HD v3 add3(v3 a, v3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RT_HD v3 sub3(v3 a, v3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RT_HD v3 mul3(v3 a, v3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RT_HD v3 div3(v3 a, v3 b) { return mk3(a.x / b.x, a.y / b.y, a.z / b.z); }
+RT_HD v3 scale3(v3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }   /* a*s and s*a */
+RT_HD v3 divs3(v3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }    /* a/s componentwise */
+RT_HD v3 neg3(v3 a) { return mk3(-a.x, -a.y, -a.z); }
+RT_HD float comp3(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+/* dot: fused chain x, then y, then z (our definition of GLSL dot) */
+RT_HD float g_dot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+RT_HD float g_dot2(v2 a, v2 b) { return fmaf(a.y, b.y, a.x * b.x); }
+RT_HD v3 g_cross(v3 a, v3 b) {
+    return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+RT_HD float g_length(v3 a) { return sqrtf(g_dot(a, a)); }
+RT_HD v3 g_normalize(v3 a) { float inv = 1.0f / sqrtf(g_dot(a, a)); return scale3(a, inv); }
+/* GLSL reflect(I,N) = I - 2*dot(N,I)*N */
+RT_HD v3 g_reflect(v3 i, v3 n) { float d2 = 2.0f * g_dot(n, i); return sub3(i, scale3(n, d2)); }
+/* GLSL refract(I,N,eta) */
+RT_HD v3 g_refract(v3 i, v3 n, float eta) {
+    float d = g_dot(n, i);
+    float k = 1.0f - (eta * eta) * (1.0f - d * d);
+    if (k < 0.0f) return mk3s(0.0f);
+    float s = eta * d + sqrtf(k);
+    return sub3(scale3(i, eta), scale3(n, s));
+}
+/* GLSL mix(x,y,a) = x*(1-a) + y*a */
+RT_HD float g_mix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+/* mat3(c0,c1,c2) * v */
+RT_HD v3 g_mat3_mul(v3 c0, v3 c1, v3 c2, v3 v) {
+    return mk3(fmaf(c2.x, v.z, fmaf(c1.x, v.y, c0.x * v.x)),
+               fmaf(c2.y, v.z, fmaf(c1.y, v.y, c0.y * v.x)),
+               fmaf(c2.z, v.z, fmaf(c1.z, v.y, c0.z * v.x)));
+}
+
+/* ------------------------------------------------------ transcendentals */
+/* sin/cos: Cody–Waite reduction by pi/2 in three fma steps (exact to ~2^-70
+ * for |x| < 2^20), then minimax polynomials on [-pi/4, pi/4]. */
+RT_HD void g_sincos(float x, float* s_out, float* c_out) {
+    float j = rintf(x * 0.636619746685028076171875f);
+    float r = fmaf(j, -1.57079637050628662109375f, x);
+    r = fmaf(j, 4.37113882867379300296306610107421875e-8f, r);
+    r = fmaf(j, 1.71512451000588190000000000e-15f, r);
+    float z = r * r;
+    float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
+    float cp = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                              4.166664568298827e-2f), z, -0.5f), z, 1.0f);
+    int q = rt_f2i(j) & 3;
+    float s, c;
+    if (q == 0)      { s = sp;  c = cp; }
+    else if (q == 1) { s = cp;  c = -sp; }
+    else if (q == 2) { s = -sp; c = -cp; }
+    else             { s = -cp; c = sp; }
+    *s_out = s; *c_out = c;
+}
+RT_HD float g_sin(float x) { float s, c; g_sincos(x, &s, &c); return s; }
+RT_HD float g_cos(float x) { float s, c; g_sincos(x, &s, &c); return c; }
+
+/* natural log: exponent/mantissa split (m in [sqrt(1/2), sqrt(2))), degree-9
+ * polynomial for log(1+f), Cody–Waite ln2 split. */
+RT_HD float g_log(float x) {
+    if (!(x == x) || x < 0.0f) return rt_u2f(0x7fc00000u);
+    if (x == 0.0f) return rt_u2f(0xff800000u);
+    if (x == rt_u2f(0x7f800000u)) return x;
+    uint32_t u = rt_f2u(x);
+    int e = 0;
+    if (u < 0x00800000u) { x = x * 8388608.0f; u = rt_f2u(x); e = -23; }
+    e += (int)(u >> 23) - 126;                 /* x = m * 2^e, m in [0.5,1) */
+    float m = rt_u2f((u & 0x007fffffu) | 0x3f000000u);
+    if (m < 0.707106781186547524f) { e -= 1; m = m + m - 1.0f; }
+    else { m = m - 1.0f; }
+    float z = m * m;
+    float y = fmaf(fmaf(fmaf(fmaf(fmaf(fmaf(fmaf(fmaf(7.0376836292e-2f, m, -1.1514610310e-1f), m,
+                  1.1676998740e-1f), m, -1.2420140846e-1f), m, 1.4249322787e-1f), m,
+                  -1.6668057665e-1f), m, 2.0000714765e-1f), m, -2.4999993993e-1f), m,
+                  3.3333331174e-1f);
+    y = (y * m) * z;
+    float fe = (float)e;
+    y = fmaf(fe, -2.12194440e-4f, y);
+    y = fmaf(-0.5f, z, y);
+    float r = m + y;
+    return fmaf(fe, 0.693359375f, r);
+}
+
+/* asin core on [0, 0.5]: x + x*z*P(z), z = x*x */
+RT_HD float rt_asin_core(float x, float z) {
+    float p = fmaf(fmaf(fmaf(fmaf(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z,
+                   7.4953002686e-2f), z, 1.6666752422e-1f);
+    return fmaf(p * z, x, x);
+}
+RT_HD float g_acos(float x) {
+    float a = fabsf(x);
+    if (!(a <= 1.0f)) return rt_u2f(0x7fc00000u);
+    if (a > 0.5f) {
+        float z = 0.5f * (1.0f - a);
+        float s = sqrtf(z);
+        float r = 2.0f * rt_asin_core(s, z);        /* acos(|x|) */
+        return (x < 0.0f) ? (3.14159274101257324f - r) + (-8.74227766e-8f) : r;
+    }
+    float p = rt_asin_core(a, a * a);
+    float asn = (x < 0.0f) ? -p : p;
+    return (1.57079637050628662f - asn) + (-4.37113883e-8f);
+}
+/* atan on all reals (range-reduced at tan(3pi/8), tan(pi/8)) */
+RT_HD float rt_atan(float x) {
+    float a = fabsf(x);
+    float y0 = 0.0f, t = a;
+    if (a > 2.414213562373095f) { y0 = 1.57079637050628662f; t = -1.0f / a; }
+    else if (a > 0.4142135623730950f) { y0 = 0.785398185253143311f; t = (a - 1.0f) / (a + 1.0f); }
+    float z = t * t;
+    float p = fmaf(fmaf(fmaf(8.05374449538e-2f, z, -1.38776856032e-1f), z, 1.99777106478e-1f), z,
+                   -3.33329491539e-1f);
+    float r = y0 + fmaf(p * z, t, t);
+    return (x < 0.0f) ? -r : r;
+}
+/* GLSL atan(y, x) with IEEE signed-zero quadrant rules (needed by the
+ * get_sphere_uv known-answer table, texture.glsl:100-102). */
+RT_HD float g_atan2(float y, float x) {
+    if (!(x == x) || !(y == y)) return rt_u2f(0x7fc00000u);
+    int yneg = (rt_f2u(y) >> 31) != 0;
+    int xneg = (rt_f2u(x) >> 31) != 0;
+    if (y == 0.0f) {
+        if (xneg) return yneg ? -3.14159274101257324f : 3.14159274101257324f;
+        return y;                                   /* ±0 */
+    }
+    if (x == 0.0f) return yneg ? -1.57079637050628662f : 1.57079637050628662f;
+    float z = rt_atan(y / x);
+    if (x < 0.0f) z = yneg ? z - 3.14159274101257324f : z + 3.14159274101257324f;
+    return z;
+}
+/* pow(x, 5.0) as used by Schlick (scatter.glsl:21) */
+RT_HD float g_pow5(float x) { float x2 = x * x; return (x2 * x2) * x; }
+
+/* unorm8 -> float, GL conversion c/255 */
+RT_HD float rt_unorm8(uint32_t c) { return (float)c / 255.0f; }
+
+#endif /* RT_GLSL_H */

@@ -1,0 +1,877 @@
+// rt_oracle.cpp — TEST INFRASTRUCTURE ONLY (see rt_oracle.h).
+//
+// A deliberately plain, scalar restatement of the reference GLSL:
+//   S/raytrace/compute.glsl         main, ray_color, trace_through_bvh,
+//                                   set_material_properties, get_ray
+//   S/utils/hitting.glsl            hit_sphere/aabb/quad/box/constant_medium
+//   S/utils/scatter.glsl            scatter and helpers
+//   S/utils/pdf.glsl                mixture-PDF pieces, light sampling
+//   S/utils/random.glsl             rand() and samplers
+//   S/utils/texture.glsl            textures, Perlin noise, sphere uv
+//   S/utils/math.glsl, interval.glsl
+// (S/ = src/main/resources/shaders/ in the reference.)  It keeps the
+// reference's structure — per-invocation globals, an int stack[64] BVH walk,
+// set_material_properties on every closer hit — so that it shares nothing with
+// the optimized HIP kernel except the GLSL built-in definitions of
+// include/rt/rt_glsl.h.  Undefined reference behaviour follows SURVEY App. A.
+#include "rt_oracle.h"
+
+#include "rt/rt_glsl.h"
+#include "rt/rt_types.h"
+
+#include <atomic>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------ scene
+struct Texture {
+    int format = 0, w = 0, h = 0;
+    const uint8_t* data = nullptr;
+    // texelFetch(sampler, ivec2(x,y), 0) — out of range reads vec4(0)
+    void fetch(int x, int y, float out[4]) const {
+        out[0] = out[1] = out[2] = out[3] = 0.0f;
+        if (!data || x < 0 || y < 0 || x >= w || y >= h) return;
+        size_t i = (size_t)y * w + x;
+        if (format == RT_TEX_RGB8) {
+            out[0] = rt_unorm8(data[i * 3]); out[1] = rt_unorm8(data[i * 3 + 1]);
+            out[2] = rt_unorm8(data[i * 3 + 2]); out[3] = 1.0f;
+        } else if (format == RT_TEX_RGBA8) {
+            for (int c = 0; c < 4; c++) out[c] = rt_unorm8(data[i * 4 + c]);
+        } else if (format == RT_TEX_R32F) {
+            float f; std::memcpy(&f, data + i * 4, 4);
+            out[0] = f; out[3] = 1.0f;
+        }
+    }
+};
+
+struct Scene {
+    const rt_sphere* spheres = nullptr; int n_spheres = 0;
+    const rt_bvh_node* nodes = nullptr; int n_nodes = 0;
+    const rt_quad* quads = nullptr; int n_quads = 0;
+    const rt_medium* media = nullptr; int n_media = 0;
+    const rt_box* boxes = nullptr; int n_boxes = 0;
+    int lights_count = 0; const int32_t* lights = nullptr;
+    Texture tex[8];
+    rt_camera_ubo cam;
+    int max_depth = 5;
+    v3 background;
+    float sqrt_spp = 1, recip_sqrt_spp = 1;
+};
+
+struct Counters {
+    oracle_counters c;
+    Counters() { std::memset(&c, 0, sizeof(c)); }
+};
+
+// ------------------------------------------------------- GLSL structs
+struct Ray { v3 o, dir; };
+struct HitRecord { bool is_front_face = false; v3 p = mk3s(0); v3 normal = mk3s(0); float t = 0; v2 uv = {0, 0}; };
+struct Interval { float min, max; };
+
+// Per-invocation state: the globals of compute.glsl:44-50 plus uniforms.
+struct Inv {
+    const Scene* S;
+    Counters* C;
+    v2 pixel_coord;
+    float rand_factor;
+    float time;
+    v3 attenuation, color_from_emission;
+    int material;
+    int frame_count;
+};
+
+// ---------------------------------------------------------- interval.glsl
+bool interval_surrounds(Interval in, float x) { return in.min < x && x < in.max; }
+bool interval_contains(Interval in, float x) { return in.min <= x && x <= in.max; }
+
+// ------------------------------------------------------------ random.glsl
+// random.glsl:2-7
+float rand(Inv& I) {
+    I.rand_factor += 0.001f;
+    v2 co = I.pixel_coord;
+    co.x += I.rand_factor;
+    co.y += I.rand_factor;
+    v2 k = {12.9898f, 78.233f};
+    if (I.C) I.C->c.rand_calls++;
+    return g_fract(g_sin(g_dot2(co, k)) * 43758.5453123f);
+}
+float rand(Inv& I, float mn, float mx) { return mn + rand(I) * (mx - mn); }          // :10-12
+int rand_int(Inv& I, int mn, int mx) { return rt_f2i(floorf(rand(I, (float)mn, (float)(mx + 1)))); }  // :15-17
+
+v3 random_in_unit_disk(Inv& I) {   // :19-24
+    while (true) {
+        float a = rand(I, -1.0f, 1.0f);
+        float b = rand(I, -1.0f, 1.0f);
+        v3 p = mk3(a, b, 0.0f);
+        if (g_dot(p, p) < 1.0f) return p;
+    }
+}
+v3 defocus_disk_sample(Inv& I) {   // :27-30
+    v3 p = random_in_unit_disk(I);
+    const rt_camera_ubo& c = I.S->cam;
+    return add3(add3(ld3(c.camera_pos), scale3(ld3(c.defocus_disk_u), p.x)), scale3(ld3(c.defocus_disk_v), p.y));
+}
+v3 rand_vec3(Inv& I, float mn, float mx) {   // :33-38
+    float r1 = rand(I, mn, mx);
+    float r2 = rand(I, mn, mx);
+    float r3 = rand(I, mn, mx);
+    return mk3(r1, r2, r3);
+}
+v3 rand_vec_in_unit_sphere(Inv& I) {   // :40-45
+    while (true) {
+        v3 p = rand_vec3(I, -1.0f, 1.0f);
+        if (g_dot(p, p) < 1.0f) return p;
+    }
+}
+v3 rand_unit_vec(Inv& I) { return g_normalize(rand_vec_in_unit_sphere(I)); }   // :47-49
+v3 rand_cosine_direction(Inv& I) {   // :59-69
+    float r1 = rand(I);
+    float r2 = rand(I);
+    float phi = 2.0f * RT_PI * r1;
+    float x = g_cos(phi) * sqrtf(r2);
+    float y = g_sin(phi) * sqrtf(r2);
+    float z = sqrtf(1.0f - r2);
+    return mk3(x, y, z);
+}
+v3 rand_to_sphere(Inv& I, float radius, float distance_squared) {   // :71-80
+    float r1 = rand(I);
+    float r2 = rand(I);
+    float z = 1.0f + r2 * (sqrtf(1.0f - radius * radius / distance_squared) - 1.0f);
+    float phi = 2.0f * RT_PI * r1;
+    float x = g_cos(phi) * sqrtf(1.0f - z * z);
+    float y = g_sin(phi) * sqrtf(1.0f - z * z);
+    return mk3(x, y, z);
+}
+v3 pixel_sample_square(Inv& I) {   // :82-100
+    const Scene& S = *I.S;
+    float sqrt_frame_count = g_mod((float)I.frame_count, S.sqrt_spp);
+    float layer = (float)I.frame_count / S.sqrt_spp;
+    float base_x = (sqrt_frame_count + 0.5f) * S.recip_sqrt_spp;
+    float base_y = (layer + 0.5f) * S.recip_sqrt_spp;
+    float jitter_x = (rand(I) - 0.5f) * S.recip_sqrt_spp;
+    float jitter_y = (rand(I) - 0.5f) * S.recip_sqrt_spp;
+    float px = base_x + jitter_x - 0.5f;
+    float py = base_y + jitter_y - 0.5f;
+    return add3(scale3(ld3(S.cam.pixel_delta_u), px), scale3(ld3(S.cam.pixel_delta_v), py));
+}
+
+// -------------------------------------------------------------- math.glsl
+v3 transform_onb(v3 vec, v3 normal) {   // math.glsl:3-12
+    v3 w = g_normalize(normal);
+    v3 a = (fabsf(w.x) > 0.9f) ? mk3(0, 1, 0) : mk3(1, 0, 0);
+    v3 v = g_normalize(g_cross(w, a));
+    v3 u = g_cross(w, v);
+    return g_mat3_mul(u, v, w, vec);
+}
+
+// ----------------------------------------------------------- texture.glsl
+v3 checkerboard(Inv& I, v3 p, int tex_idx, int pix_idx) {   // :6-17
+    const Texture& T = I.S->tex[tex_idx & 7];
+    float t[4];
+    T.fetch(pix_idx + 2, 0, t);
+    float scale = t[0];
+    float inv_scale = 1.0f / scale;
+    v3 q = scale3(p, inv_scale);
+    int ix = rt_f2i(q.x), iy = rt_f2i(q.y), iz = rt_f2i(q.z);
+    bool is_even = ((ix + iy + iz) % 2) == 0;
+    if (I.C) I.C->c.texel_bytes += 6;
+    if (is_even) { T.fetch(pix_idx, 0, t); return mk3(t[0], t[1], t[2]); }
+    T.fetch(pix_idx + 1, 0, t);
+    return mk3(t[0], t[1], t[2]);
+}
+
+float perlin_interp(const v3 c[2][2][2], float u, float v, float w) {   // :19-36
+    float uu = u * u * (3.0f - 2.0f * u);
+    float vv = v * v * (3.0f - 2.0f * v);
+    float ww = w * w * (3.0f - 2.0f * w);
+    float accum = 0.0f;
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++)
+            for (int k = 0; k < 2; k++) {
+                v3 weight_v = mk3(u - (float)i, v - (float)j, w - (float)k);
+                float fi = (float)i, fj = (float)j, fk = (float)k;
+                accum += (fi * uu + (1.0f - fi) * (1.0f - uu)) * (fj * vv + (1.0f - fj) * (1.0f - vv)) *
+                         (fk * ww + (1.0f - fk) * (1.0f - ww)) * g_dot(c[i][j][k], weight_v);
+            }
+    return accum;
+}
+
+float noise(const Texture& T, v3 p) {   // :38-77
+    float u = p.x - floorf(p.x);
+    float v = p.y - floorf(p.y);
+    float w = p.z - floorf(p.z);
+    u = u * u * (3.0f - 2.0f * u);
+    v = v * v * (3.0f - 2.0f * v);
+    w = w * w * (3.0f - 2.0f * w);
+    int i = rt_f2i(floorf(p.x));
+    int j = rt_f2i(floorf(p.y));
+    int k = rt_f2i(floorf(p.z));
+    v3 c[2][2][2];
+    float t[4];
+    for (int di = 0; di < 2; di++)
+        for (int dj = 0; dj < 2; dj++)
+            for (int dk = 0; dk < 2; dk++) {
+                T.fetch(3, (i + di) & 255, t); int perm_x = rt_f2i(t[0]);
+                T.fetch(4, (j + dj) & 255, t); int perm_y = rt_f2i(t[0]);
+                T.fetch(5, (k + dk) & 255, t); int perm_z = rt_f2i(t[0]);
+                int idx = perm_x ^ perm_y ^ perm_z;
+                float cx, cy, cz;
+                T.fetch(0, idx, t); cx = t[0];
+                T.fetch(1, idx, t); cy = t[0];
+                T.fetch(2, idx, t); cz = t[0];
+                c[di][dj][dk] = mk3(cx, cy, cz);
+            }
+    return perlin_interp(c, u, v, w);
+}
+
+float noise_turb(const Texture& T, v3 p, int depth) {   // :79-90
+    float accum = 0.0f;
+    float weight = 1.0f;
+    for (int i = 0; i < depth; i++) {
+        accum += weight * noise(T, p);
+        weight *= 0.5f;
+        p = scale3(p, 2.0f);
+    }
+    return fabsf(accum);
+}
+
+v3 perlin_noise_color(Inv& I, v3 p, float scale, int tex_idx) {   // :92-94
+    if (I.C) I.C->c.texel_bytes += 7 * 8 * 6 * 4;
+    float s = 1.0f + g_sin(scale * p.z + 10.0f * noise_turb(I.S->tex[tex_idx & 7], p, 7));
+    return mk3s(0.5f * s);
+}
+
+v2 get_sphere_uv(v3 p) {   // :96-110
+    p = g_normalize(p);
+    float theta = g_acos(-p.y);
+    float phi = g_atan2(-p.z, p.x) + RT_PI;
+    v2 r = {phi / (2.0f * RT_PI), theta / RT_PI};
+    return r;
+}
+
+// texture2D with GL_LINEAR + CLAMP_TO_EDGE (Texture.java:74-77)
+v3 texture_bilinear(const Texture& T, v2 uv) {
+    if (!T.data || T.w <= 0 || T.h <= 0) return mk3s(0.0f);
+    float x = uv.x * (float)T.w - 0.5f;
+    float y = uv.y * (float)T.h - 0.5f;
+    float fx = floorf(x), fy = floorf(y);
+    float a = x - fx, b = y - fy;
+    int x0 = rt_f2i(fx), y0 = rt_f2i(fy);
+    auto clampi = [](int i, int n) { return i < 0 ? 0 : (i > n - 1 ? n - 1 : i); };
+    int x1 = clampi(x0 >= T.w - 1 ? T.w - 1 : x0 + 1, T.w);
+    int y1 = clampi(y0 >= T.h - 1 ? T.h - 1 : y0 + 1, T.h);
+    x0 = clampi(x0, T.w); y0 = clampi(y0, T.h);
+    float t00[4], t10[4], t01[4], t11[4];
+    T.fetch(x0, y0, t00); T.fetch(x1, y0, t10); T.fetch(x0, y1, t01); T.fetch(x1, y1, t11);
+    float r[3];
+    for (int c = 0; c < 3; c++)
+        r[c] = (t00[c] * (1.0f - a) + t10[c] * a) * (1.0f - b) + (t01[c] * (1.0f - a) + t11[c] * a) * b;
+    return mk3(r[0], r[1], r[2]);
+}
+
+v3 texture_color(Inv& I, v3 p, int id, v2 uv) {   // :112-132
+    int detail_i = id & 0xFFF;
+    int index = (id >> 12) & 0xFFFF;
+    int texture_type = (id >> 28) & 0xF;
+    float detail_f = (float)detail_i / 4095.0f;
+    switch (texture_type) {
+        case RT_TEXTYPE_CHECKER: return checkerboard(I, p, index, detail_i * 3);
+        case RT_TEXTYPE_IMAGE:
+            if (I.C) I.C->c.texel_bytes += 12;
+            return texture_bilinear(I.S->tex[index & 7], uv);
+        case RT_TEXTYPE_PERLIN: return perlin_noise_color(I, p, detail_f * 100.0f, index);
+        case RT_TEXTYPE_SOLID: {
+            if (I.C) I.C->c.texel_bytes += 3;
+            float t[4];
+            I.S->tex[index & 7].fetch(detail_i, 0, t);
+            return mk3(t[0], t[1], t[2]);
+        }
+        default: return mk3s(0.0f);
+    }
+}
+
+// ----------------------------------------------------------- hitting.glsl
+bool is_front_face(v3 ray_dir, v3 outward_normal) { return g_dot(ray_dir, outward_normal) < 0.0f; }   // :4-7
+v3 get_face_normal(v3 outward_normal, bool front) { return front ? outward_normal : neg3(outward_normal); }
+v3 sphere_center(const Inv& I, v3 c1, v3 cv) { return add3(c1, scale3(cv, I.time)); }   // :13-15
+
+bool hit_sphere(Inv& I, const Ray& ray, Interval ray_t, const rt_sphere& sphere, HitRecord& rec) {   // :17-47
+    v3 center = sphere_center(I, ld3(sphere.center1), ld3(sphere.center_vec));
+    v3 oc = sub3(ray.o, center);
+    float a = g_dot(ray.dir, ray.dir);
+    float half_b = g_dot(oc, ray.dir);
+    float c = g_dot(oc, oc) - sphere.radius * sphere.radius;
+    float discriminant = half_b * half_b - a * c;
+    if (discriminant < 0.0f) return false;
+    float sqrtd = sqrtf(discriminant);
+    float root = (-half_b - sqrtd) / a;
+    if (!interval_surrounds(ray_t, root)) {
+        root = (-half_b + sqrtd) / a;
+        if (!interval_surrounds(ray_t, root)) return false;
+    }
+    rec.t = root;
+    rec.p = add3(ray.o, scale3(ray.dir, rec.t));
+    v3 outward_normal = divs3(sub3(rec.p, center), sphere.radius);
+    rec.is_front_face = is_front_face(ray.dir, outward_normal);
+    rec.normal = get_face_normal(outward_normal, rec.is_front_face);
+    rec.uv = get_sphere_uv(sub3(rec.p, center));
+    return true;
+}
+
+Interval axis_interval(int n, const rt_bvh_node& nd) {   // :49-53
+    if (n == 1) return Interval{nd.ymin, nd.ymax};
+    if (n == 2) return Interval{nd.zmin, nd.zmax};
+    return Interval{nd.xmin, nd.xmax};
+}
+
+bool hit_aabb(const Ray& ray, Interval ray_t, const rt_bvh_node& nd) {   // :55-76
+    for (int axis = 0; axis < 3; axis++) {
+        Interval ax = axis_interval(axis, nd);
+        float adinv = 1.0f / comp3(ray.dir, axis);
+        float t0 = (ax.min - comp3(ray.o, axis)) * adinv;
+        float t1 = (ax.max - comp3(ray.o, axis)) * adinv;
+        if (t0 < t1) {
+            if (t0 > ray_t.min) ray_t.min = t0;
+            if (t1 < ray_t.max) ray_t.max = t1;
+        } else {
+            if (t1 > ray_t.min) ray_t.min = t1;
+            if (t0 < ray_t.max) ray_t.max = t0;
+        }
+        if (ray_t.max <= ray_t.min) return false;
+    }
+    return true;
+}
+
+bool is_interior(float a, float b, v2& uv) {   // :78-88
+    Interval unit = {0.0f, 1.0f};
+    if (!interval_contains(unit, a) || !interval_contains(unit, b)) return false;
+    uv.x = a; uv.y = b;
+    return true;
+}
+
+bool hit_quad(const Ray& ray, Interval ray_t, const rt_quad& quad, HitRecord& rec) {   // :90-133
+    v3 normal = ld3(quad.normal);
+    float denom = g_dot(normal, ray.dir);
+    if (fabsf(denom) < 1e-8f) return false;
+    float t = (quad.d - g_dot(normal, ray.o)) / denom;
+    if (!interval_contains(ray_t, t)) return false;
+    v3 intersection = add3(ray.o, scale3(ray.dir, t));
+    v3 ph = sub3(intersection, ld3(quad.q));
+    v3 u = ld3(quad.u), v = ld3(quad.v);
+    float delta, alpha, beta;
+    if ((delta = u.x * v.y - u.y * v.x) != 0.0f) {
+        alpha = (ph.x * v.y - ph.y * v.x) / delta;
+        beta = (ph.y * u.x - ph.x * u.y) / delta;
+    } else if ((delta = u.x * v.z - u.z * v.x) != 0.0f) {
+        alpha = (ph.x * v.z - ph.z * v.x) / delta;
+        beta = (ph.z * u.x - ph.x * u.z) / delta;
+    } else {
+        delta = u.y * v.z - u.z * v.y;
+        alpha = (ph.y * v.z - ph.z * v.y) / delta;
+        beta = (ph.z * u.y - ph.y * u.z) / delta;
+    }
+    if (!is_interior(alpha, beta, rec.uv)) return false;
+    rec.t = t;
+    rec.p = intersection;
+    rec.is_front_face = is_front_face(ray.dir, normal);
+    rec.normal = get_face_normal(normal, rec.is_front_face);
+    return true;
+}
+
+bool hit_box(const Ray& ray, Interval ray_t, const rt_box& box, HitRecord& rec) {   // :135-146
+    bool has_hit = false;
+    for (int i = 0; i < 6; i++) {
+        if (hit_quad(ray, ray_t, box.quads[i], rec)) {
+            ray_t.max = rec.t;
+            has_hit = true;
+        }
+    }
+    return has_hit;
+}
+
+bool hit_boundary(Inv& I, const Ray& ray, Interval ray_t, int idx, int type, HitRecord& rec) {   // :148-160
+    const Scene& S = *I.S;
+    switch (type) {
+        case RT_MODEL_SPHERE:
+            if (I.C) { I.C->c.sphere_tests++; I.C->c.prim_bytes += 48; }
+            return hit_sphere(I, ray, ray_t, S.spheres[idx], rec);
+        case RT_MODEL_QUAD:
+            if (I.C) { I.C->c.quad_tests++; I.C->c.prim_bytes += 80; }
+            return hit_quad(ray, ray_t, S.quads[idx], rec);
+        case RT_MODEL_BOX:
+            if (I.C) { I.C->c.box_tests++; I.C->c.prim_bytes += 480; }
+            return hit_box(ray, ray_t, S.boxes[idx], rec);
+        default: return false;
+    }
+}
+
+bool hit_constant_medium(Inv& I, const Ray& ray, Interval ray_t, const rt_medium& medium, HitRecord& rec) {   // :162-193
+    HitRecord rec1, rec2;
+    if (!hit_boundary(I, ray, Interval{-RT_INFINITY, RT_INFINITY}, medium.boundary_idx, medium.boundary_type, rec1))
+        return false;
+    if (!hit_boundary(I, ray, Interval{rec1.t + 0.0001f, RT_INFINITY}, medium.boundary_idx, medium.boundary_type, rec2))
+        return false;
+    if (rec1.t < ray_t.min) rec1.t = ray_t.min;
+    if (rec2.t > ray_t.max) rec2.t = ray_t.max;
+    if (rec1.t >= rec2.t) return false;
+    if (rec1.t < 0.0f) rec1.t = 0.0f;
+    float ray_length = g_length(ray.dir);
+    float distance_inside_boundary = (rec2.t - rec1.t) * ray_length;
+    float hit_distance = medium.neg_inv_density * g_log(rand(I));
+    if (hit_distance > distance_inside_boundary) return false;
+    rec.t = rec1.t + hit_distance / ray_length;
+    rec.p = add3(ray.o, scale3(ray.dir, rec.t));
+    rec.normal = mk3(1.0f, 0.0f, 0.0f);
+    rec.is_front_face = true;
+    return true;
+}
+
+bool hit_model(Inv& I, const Ray& ray, Interval ray_t, int idx, int type, HitRecord& rec) {   // :195-206
+    if (hit_boundary(I, ray, ray_t, idx, type, rec)) return true;
+    if (type == RT_MODEL_CONSTANT_MEDIUM) {
+        if (I.C) { I.C->c.medium_tests++; I.C->c.prim_bytes += 20; }
+        return hit_constant_medium(I, ray, ray_t, I.S->media[idx], rec);
+    }
+    return false;
+}
+
+// --------------------------------------------------------------- pdf.glsl
+float sphere_pdf_value() { return 1.0f / (4.0f * RT_PI); }   // :3-5
+
+float sphere_model_pdf(Inv& I, v3 origin, v3 direction, const rt_sphere& sphere) {   // :11-24
+    HitRecord rec;
+    Ray r{origin, direction};
+    if (!hit_sphere(I, r, Interval{0.001f, RT_INFINITY}, sphere, rec)) return 0.0f;
+    v3 pc = sub3(ld3(sphere.center1), origin);
+    float distance_squared = g_dot(pc, pc);
+    float cos_theta_max = sqrtf(1.0f - sphere.radius * sphere.radius / distance_squared);
+    float solid_angle = 2.0f * RT_PI * (1.0f - cos_theta_max);
+    return 1.0f / solid_angle;
+}
+
+v3 sphere_model_random(Inv& I, v3 origin, v3 center, float radius) {   // :26-30
+    v3 direction = sub3(center, origin);
+    float distance_squared = g_dot(direction, direction);
+    return transform_onb(rand_to_sphere(I, radius, distance_squared), direction);
+}
+
+float cosine_pdf_value(v3 direction, v3 normal) {   // :32-35  (normalize(float) = sign, Q2)
+    float cos_theta = g_normalize1(g_dot(direction, normal));
+    return g_max(0.0f, cos_theta / RT_PI);
+}
+
+v3 cosine_generate_direction(Inv& I, v3 normal) { return transform_onb(rand_cosine_direction(I), normal); }   // :37-39
+
+float quad_pdf_value(v3 origin, v3 direction, const rt_quad& quad) {   // :41-51
+    HitRecord rec;
+    Ray r{origin, direction};
+    if (!hit_quad(r, Interval{0.001f, RT_INFINITY}, quad, rec)) return 0.0f;
+    float distance_squared = rec.t * rec.t * g_dot(direction, direction);
+    float cosine = fabsf(g_dot(direction, rec.normal) / g_length(direction));
+    return distance_squared / (cosine * quad.area);
+}
+
+v3 quad_random(Inv& I, v3 origin, const rt_quad& quad) {   // :53-56
+    float r1 = rand(I);
+    v3 p = add3(ld3(quad.q), scale3(ld3(quad.u), r1));
+    float r2 = rand(I);
+    p = add3(p, scale3(ld3(quad.v), r2));
+    return sub3(p, origin);
+}
+
+float lights_pdf_value(Inv& I, v3 origin, v3 direction) {   // :58-81
+    const Scene& S = *I.S;
+    float weight = 1.0f / (float)S.lights_count;
+    float sum = 0.0f;
+    if (I.C) I.C->c.light_bytes += 4;
+    for (int i = 0; i < S.lights_count; i++) {
+        int type = (S.lights[i] >> 16) & 0xFFFF;
+        int idx = S.lights[i] & 0xFFFF;
+        float pdf_value = 0.0f;
+        if (type == RT_MODEL_SPHERE) {
+            if (I.C) I.C->c.light_bytes += 4 + 48;
+            pdf_value = sphere_model_pdf(I, origin, direction, S.spheres[idx]);
+        } else if (type == RT_MODEL_QUAD) {
+            if (I.C) I.C->c.light_bytes += 4 + 80;
+            pdf_value = quad_pdf_value(origin, direction, S.quads[idx]);
+        }
+        sum += weight * pdf_value;
+    }
+    return sum;
+}
+
+v3 lights_random(Inv& I, v3 origin) {   // :83-96 (no-light / unknown type: vec3(0), Q1)
+    const Scene& S = *I.S;
+    int li = rand_int(I, 0, S.lights_count - 1);
+    if (I.C) I.C->c.light_bytes += 8;
+    if (li < 0 || li >= S.lights_count) return mk3s(0.0f);
+    int hittable = S.lights[li];
+    int type = (hittable >> 16) & 0xFFFF;
+    int idx = hittable & 0xFFFF;
+    if (type == RT_MODEL_SPHERE) {
+        if (I.C) I.C->c.light_bytes += 48;
+        return sphere_model_random(I, origin, ld3(S.spheres[idx].center1), S.spheres[idx].radius);
+    }
+    if (type == RT_MODEL_QUAD) {
+        if (I.C) I.C->c.light_bytes += 80;
+        return quad_random(I, origin, S.quads[idx]);
+    }
+    return mk3s(0.0f);
+}
+
+float material_pdf_value(v3 direction, int material_val, v3 normal) {   // :98-109
+    int id = (material_val >> 16) & 0xFFFF;
+    if (id == RT_MAT_LAMBERTIAN) return cosine_pdf_value(direction, normal);
+    if (id == RT_MAT_ISOTROPIC) return sphere_pdf_value();
+    return 0.0f;
+}
+
+float scattering_pdf(v3 normal, v3 scatter_dir, int material_val) {   // :111-124
+    int id = (material_val >> 16) & 0xFFFF;
+    if (id == RT_MAT_LAMBERTIAN) {
+        float cos_theta = g_dot(normal, g_normalize(scatter_dir));
+        return g_max(0.0f, cos_theta / RT_PI);
+    }
+    if (id == RT_MAT_ISOTROPIC) return 1.0f / (4.0f * RT_PI);
+    return 0.0f;
+}
+
+// ----------------------------------------------------------- scatter.glsl
+bool near_zero(v3 v) { const float s = 1e-8f; return fabsf(v.x) < s && fabsf(v.y) < s && fabsf(v.z) < s; }
+
+void metal_scatter(Inv& I, v3& ray_dir, v3 normal, float fuzz) {   // :12-15
+    ray_dir = g_reflect(ray_dir, normal);
+    v3 n = g_normalize(ray_dir);
+    ray_dir = add3(n, scale3(rand_unit_vec(I), fuzz));
+}
+
+float reflectance(float cos_theta, float eta) {   // :17-22
+    float r0 = (1.0f - eta) / (1.0f + eta);
+    r0 = r0 * r0;
+    return r0 + (1.0f - r0) * g_pow5(1.0f - cos_theta);
+}
+
+void refract_scatter(Inv& I, v3& ray_dir, v3 normal, float eta) {   // :24-37
+    ray_dir = g_normalize(ray_dir);
+    float cos_theta = g_min(g_dot(neg3(ray_dir), normal), 1.0f);
+    float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+    bool cannot_refract = eta * sin_theta > 1.0f;
+    if (cannot_refract || reflectance(cos_theta, eta) > rand(I)) ray_dir = g_reflect(ray_dir, normal);
+    else ray_dir = g_refract(ray_dir, normal, eta);
+}
+
+bool scatter(Inv& I, Ray& ray, v3 hit_point, v3 normal, bool front, int material_val, bool& skip_pdf) {   // :43-98
+    int material_id = (material_val >> 16) & 0xFFFF;
+    bool should_scatter = false;
+    switch (material_id) {
+        case RT_MAT_LAMBERTIAN:
+            ray.dir = cosine_generate_direction(I, normal);
+            should_scatter = true; skip_pdf = false;
+            break;
+        case RT_MAT_METAL: {
+            float fuzz = (float)(material_val & 0xFFFF) / 65535.0f;
+            metal_scatter(I, ray.dir, normal, fuzz);
+            should_scatter = g_dot(ray.dir, normal) > 0.0f;
+            skip_pdf = true;
+            break;
+        }
+        case RT_MAT_DIELECTRIC: {
+            float nior = (float)(material_val & 0xFFFF) / 65535.0f;
+            float eta = g_mix(1.0f, 2.5f, nior);
+            if (front) eta = 1.0f / eta;
+            refract_scatter(I, ray.dir, normal, eta);
+            should_scatter = true; skip_pdf = true;
+            break;
+        }
+        case RT_MAT_DIFFUSE_LIGHT:
+            return false;
+        case RT_MAT_ISOTROPIC:
+            ray.o = hit_point;
+            ray.dir = rand_unit_vec(I);
+            should_scatter = true; skip_pdf = false;
+            break;
+        default:
+            break;
+    }
+    if (near_zero(ray.dir)) ray.dir = normal;
+    return should_scatter;
+}
+
+// ----------------------------------------------------------- compute.glsl
+void set_material_properties(Inv& I, int idx, int type, v3 p, v2 uv, bool front) {   // :197-224
+    const Scene& S = *I.S;
+    switch (type) {
+        case RT_MODEL_SPHERE: {
+            const rt_sphere& s = S.spheres[idx];
+            if (I.C) I.C->c.material_bytes += 48;
+            I.material = s.material;
+            I.attenuation = texture_color(I, p, s.texture_id, uv);
+            I.color_from_emission = front ? ld3(s.emission) : mk3s(0.0f);
+            return;
+        }
+        case RT_MODEL_QUAD: {
+            const rt_quad& q = S.quads[idx];
+            if (I.C) I.C->c.material_bytes += 80;
+            I.material = q.material;
+            I.attenuation = texture_color(I, p, q.texture_id, uv);
+            I.color_from_emission = front ? ld3(q.emission) : mk3s(0.0f);
+            return;
+        }
+        case RT_MODEL_CONSTANT_MEDIUM: {
+            const rt_medium& m = S.media[idx];
+            if (I.C) I.C->c.material_bytes += 20;
+            I.material = m.phase_material;
+            I.attenuation = texture_color(I, p, m.texture_id, uv);
+            I.color_from_emission = mk3s(0.0f);
+            return;
+        }
+        case RT_MODEL_BOX: {
+            const rt_quad& q = S.boxes[idx].quads[0];
+            if (I.C) I.C->c.material_bytes += 480;
+            I.material = q.material;
+            I.attenuation = texture_color(I, p, q.texture_id, uv);
+            I.color_from_emission = front ? ld3(q.emission) : mk3s(0.0f);
+            return;
+        }
+    }
+}
+
+bool trace_through_bvh(Inv& I, const Ray& ray, Interval ray_t, HitRecord& rec) {   // :226-266
+    const Scene& S = *I.S;
+    if (S.n_nodes == 0) return false;
+    int stack[64];
+    int sp = 0;
+    stack[sp++] = 0;
+    bool has_hit = false;
+    while (sp > 0) {
+        int node_idx = stack[--sp];
+        const rt_bvh_node& node = S.nodes[node_idx];
+        if (I.C) { I.C->c.node_visits++; I.C->c.node_bytes += 32; }
+        if (hit_aabb(ray, ray_t, node)) {
+            int node_type = node.left_id & 0xFFFF;
+            if (node_type != 0) {
+                int model_idx = (node.left_id >> 16) & 0xFFFF;
+                for (int i = 0; i < 2; i++) {
+                    if (hit_model(I, ray, ray_t, model_idx, node_type, rec)) {
+                        has_hit = true;
+                        ray_t.max = rec.t;
+                        set_material_properties(I, model_idx, node_type, rec.p, rec.uv, rec.is_front_face);
+                    }
+                    model_idx = (node.right_id >> 16) & 0xFFFF;
+                    node_type = node.right_id & 0xFFFF;
+                }
+            } else {
+                if (sp + 2 > 64) return has_hit;   // the reference would overflow its stack
+                stack[sp++] = (node.left_id >> 16) & 0xFFFF;
+                stack[sp++] = (node.right_id >> 16) & 0xFFFF;
+            }
+        }
+    }
+    return has_hit;
+}
+
+Ray get_ray(Inv& I) {   // :268-296
+    const rt_camera_ubo& c = I.S->cam;
+    v3 coord = ld3(c.up_left);
+    coord = add3(coord, scale3(ld3(c.pixel_delta_u), I.pixel_coord.x));
+    coord = add3(coord, scale3(ld3(c.pixel_delta_v), I.pixel_coord.y));
+    coord = add3(coord, pixel_sample_square(I));
+    Ray ray;
+    ray.o = (c.defocus_angle <= 0.0f) ? ld3(c.camera_pos) : defocus_disk_sample(I);
+    ray.dir = sub3(coord, ray.o);
+    return ray;
+}
+
+v3 ray_color(Inv& I, Ray ray) {   // :298-343
+    const Scene& S = *I.S;
+    v3 final_color = mk3s(0.0f);
+    v3 acc = mk3s(1.0f);
+    HitRecord rec;
+    for (int i = 0; i < S.max_depth; i++) {
+        if (I.C) I.C->c.bounces++;
+        if (!trace_through_bvh(I, ray, Interval{0.001f, RT_INFINITY}, rec)) {
+            final_color = mul3(acc, S.background);
+            break;
+        }
+        bool skip_pdf = false;
+        if (!scatter(I, ray, rec.p, rec.normal, rec.is_front_face, I.material, skip_pdf)) {
+            final_color = mul3(acc, I.color_from_emission);
+            break;
+        }
+        ray.o = rec.p;
+        if (skip_pdf) {
+            acc = mul3(acc, I.attenuation);
+            continue;
+        }
+        if (rand(I) < 0.5f) ray.dir = lights_random(I, ray.o);
+        float lpdf = lights_pdf_value(I, ray.o, ray.dir);
+        float pdf_value = 0.5f * lpdf + 0.5f * material_pdf_value(ray.dir, I.material, rec.normal);
+        if (pdf_value == 0.0f) {
+            final_color = mul3(acc, I.color_from_emission);
+            break;
+        }
+        float sp = scattering_pdf(rec.normal, ray.dir, I.material);
+        acc = mul3(acc, divs3(scale3(I.attenuation, sp), pdf_value));
+    }
+    return final_color;
+}
+
+// compute.glsl:345-358, one invocation, one frame
+void shade_pixel(const Scene& S, Counters* C, int x, int y, int frame_count, float u_rand_factor, float* px) {
+    Inv I;
+    I.S = &S; I.C = C;
+    I.pixel_coord = {(float)x, (float)y};
+    I.rand_factor = u_rand_factor;
+    I.frame_count = frame_count;
+    I.attenuation = mk3s(0.0f); I.color_from_emission = mk3s(0.0f); I.material = 0;
+    I.time = rand(I);
+    Ray ray = get_ray(I);
+    v3 prev = mk3(px[0], px[1], px[2]);
+    v3 cur = ray_color(I, ray);
+    float n1 = (float)(frame_count - 1), n = (float)frame_count;
+    px[0] = (prev.x * n1 + cur.x) / n;
+    px[1] = (prev.y * n1 + cur.y) / n;
+    px[2] = (prev.z * n1 + cur.z) / n;
+    px[3] = 1.0f;
+    if (C) { C->c.samples++; C->c.framebuffer_bytes += 32; }
+}
+
+bool make_scene(const oracle_scene_desc* d, Scene& S) {
+    S.spheres = (const rt_sphere*)d->buf[0]; S.n_spheres = (int)(d->nbytes[0] / sizeof(rt_sphere));
+    S.nodes = (const rt_bvh_node*)d->buf[1]; S.n_nodes = (int)(d->nbytes[1] / sizeof(rt_bvh_node));
+    S.quads = (const rt_quad*)d->buf[2]; S.n_quads = (int)(d->nbytes[2] / sizeof(rt_quad));
+    S.media = (const rt_medium*)d->buf[3]; S.n_media = (int)(d->nbytes[3] / sizeof(rt_medium));
+    S.boxes = (const rt_box*)d->buf[4]; S.n_boxes = (int)(d->nbytes[4] / sizeof(rt_box));
+    if (d->nbytes[5] >= 4) {
+        const int32_t* L = (const int32_t*)d->buf[5];
+        S.lights_count = L[0];
+        S.lights = L + 1;
+        if ((size_t)(S.lights_count + 1) * 4 > d->nbytes[5]) return false;
+    }
+    for (int i = 0; i < 8; i++) {
+        S.tex[i].format = d->tex_format[i]; S.tex[i].w = d->tex_w[i]; S.tex[i].h = d->tex_h[i];
+        S.tex[i].data = (const uint8_t*)d->tex[i];
+    }
+    std::memcpy(&S.cam, d->camera, sizeof(rt_camera_ubo));
+    S.max_depth = d->max_depth;
+    S.background = mk3(d->background[0], d->background[1], d->background[2]);
+    S.sqrt_spp = d->sqrt_spp; S.recip_sqrt_spp = d->recip_sqrt_spp;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oracle_render(const oracle_scene_desc* d, int width, int height, float* rgba, int first_frame, int n_frames,
+                  const float* rand_factors, int rank, int world, int stripe_rows, int nthreads,
+                  oracle_counters* counters) {
+    if (!d || !rgba || width <= 0 || height <= 0 || n_frames < 0 || (n_frames > 0 && !rand_factors)) return -1;
+    if (world < 1 || rank < 0 || rank >= world || stripe_rows < 1 || first_frame < 1) return -1;
+    Scene S;
+    if (!make_scene(d, S)) return -1;
+    const int T = 16;
+    int tiles_x = (width + T - 1) / T, tiles_y = (height + T - 1) / T;
+    int n_tiles = tiles_x * tiles_y;
+    if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+    if (nthreads <= 0) nthreads = 1;
+    std::atomic<int> next{0};
+    std::vector<Counters> per(nthreads);
+    auto worker = [&](int tid) {
+        Counters* C = counters ? &per[tid] : nullptr;
+        for (;;) {
+            int t = next.fetch_add(1);
+            if (t >= n_tiles) break;
+            int tx = t % tiles_x, ty = t / tiles_x;
+            for (int y = ty * T; y < std::min(height, ty * T + T); y++) {
+                if ((y / stripe_rows) % world != rank) continue;
+                for (int x = tx * T; x < std::min(width, tx * T + T); x++) {
+                    float* px = rgba + ((size_t)y * width + x) * 4;
+                    for (int f = 0; f < n_frames; f++) shade_pixel(S, C, x, y, first_frame + f, rand_factors[f], px);
+                }
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < nthreads; i++) th.emplace_back(worker, i);
+    worker(0);
+    for (auto& t : th) t.join();
+    if (counters) {
+        std::memset(counters, 0, sizeof(*counters));
+        for (auto& p : per) {
+            const uint64_t* s = (const uint64_t*)&p.c;
+            uint64_t* dst = (uint64_t*)counters;
+            for (size_t k = 0; k < sizeof(oracle_counters) / 8; k++) dst[k] += s[k];
+        }
+    }
+    return 0;
+}
+
+void oracle_get_sphere_uv(float x, float y, float z, float* u, float* v) {
+    v2 r = get_sphere_uv(mk3(x, y, z));
+    *u = r.x; *v = r.y;
+}
+
+void oracle_rand_sequence(float px, float py, float f, int n, float* out) {
+    Scene S;
+    Inv I;
+    I.S = &S; I.C = nullptr; I.pixel_coord = {px, py}; I.rand_factor = f;
+    for (int i = 0; i < n; i++) out[i] = rand(I);
+}
+
+void oracle_eval_builtin(int fn, const float* x, const float* y2, float* out, int n) {
+    for (int i = 0; i < n; i++) {
+        switch (fn) {
+            case 0: out[i] = g_sin(x[i]); break;
+            case 1: out[i] = g_cos(x[i]); break;
+            case 2: out[i] = g_log(x[i]); break;
+            case 3: out[i] = g_acos(x[i]); break;
+            case 4: out[i] = g_atan2(x[i], y2 ? y2[i] : 1.0f); break;
+            case 5: out[i] = g_fract(x[i]); break;
+            case 6: out[i] = sqrtf(x[i]); break;
+            default: out[i] = 0.0f;
+        }
+    }
+}
+
+float oracle_perlin_turb(const float* table, float px, float py, float pz, int depth) {
+    Texture T;
+    T.format = RT_TEX_R32F; T.w = 6; T.h = 256; T.data = (const uint8_t*)table;
+    return noise_turb(T, mk3(px, py, pz), depth);
+}
+
+int oracle_hit_sphere(const void* sphere48, float time, const float o[3], const float dir[3], float tmin, float tmax,
+                      float* t, float p[3], float n[3], int* front) {
+    Scene S;
+    Inv I; I.S = &S; I.C = nullptr; I.time = time;
+    rt_sphere sp; std::memcpy(&sp, sphere48, sizeof(sp));
+    HitRecord rec;
+    Ray r{ld3(o), ld3(dir)};
+    if (!hit_sphere(I, r, Interval{tmin, tmax}, sp, rec)) return 0;
+    *t = rec.t; p[0] = rec.p.x; p[1] = rec.p.y; p[2] = rec.p.z;
+    n[0] = rec.normal.x; n[1] = rec.normal.y; n[2] = rec.normal.z; *front = rec.is_front_face;
+    return 1;
+}
+
+int oracle_hit_quad(const void* quad80, const float o[3], const float dir[3], float tmin, float tmax, float* t,
+                    float p[3], float n[3], int* front) {
+    rt_quad q; std::memcpy(&q, quad80, sizeof(q));
+    HitRecord rec;
+    Ray r{ld3(o), ld3(dir)};
+    if (!hit_quad(r, Interval{tmin, tmax}, q, rec)) return 0;
+    *t = rec.t; p[0] = rec.p.x; p[1] = rec.p.y; p[2] = rec.p.z;
+    n[0] = rec.normal.x; n[1] = rec.normal.y; n[2] = rec.normal.z; *front = rec.is_front_face;
+    return 1;
+}
+
+int oracle_hit_aabb(const float b[6], const float o[3], const float dir[3], float tmin, float tmax) {
+    rt_bvh_node nd{};
+    nd.xmin = b[0]; nd.xmax = b[1]; nd.ymin = b[2]; nd.ymax = b[3]; nd.zmin = b[4]; nd.zmax = b[5];
+    Ray r{ld3(o), ld3(dir)};
+    return hit_aabb(r, Interval{tmin, tmax}, nd) ? 1 : 0;
+}
+
+}  // extern "C"

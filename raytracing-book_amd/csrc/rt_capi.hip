@@ -1,0 +1,655 @@
+// rt_capi.hip — implementation of include/rt/rt.h (the drop-in C ABI).
+//
+// Host-side responsibilities that the reference's Java/GL layer had:
+// buffer/texture upload (BufferObject.uploadData, Texture.putData), uniforms
+// (ShaderProgram.setUniform*), dispatch (RaytraceExecutor.raytrace), readback
+// (glGetTexImage) and timing (QueryTimer).  Plus the MI355X-specific parts:
+// the threaded-BVH re-layout, RGB8->RGBA8 texture expansion, stripe
+// partitioning across devices/processes and caller-owned device images.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt/rt.h"
+#include "rt/rt_debug.h"
+#include "rt/rt_types.h"
+#include "rt_device.h"
+
+namespace {
+
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct Device {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = true;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    bool timed = false;
+    DevBuf nodes, spheres, quads, boxes, media, lights, tex[8];
+    DevBuf image;            // internal image
+    DevBuf args;             // rt_kernel_args slot in device memory
+    float* image_ptr = nullptr;  // active image (internal or bound)
+    bool image_bound = false;
+    int rank = 0, world = 1;     // stripe assignment of this device
+    int local_rows = 0, padded_rows = 0;
+};
+
+}  // namespace
+
+struct rt_ctx {
+    std::vector<Device> devs;
+    std::string err;
+    // host copies of what the kernel needs
+    std::vector<uint8_t> host_buf[6];
+    bool uploaded[6] = {false, false, false, false, false, false};
+    int tex_format[8] = {0}, tex_w[8] = {0}, tex_h[8] = {0};
+    rt_camera_ubo cam{};
+    bool have_cam = false;
+    int max_depth = 5;
+    float background[3] = {0, 0, 0};
+    float sqrt_spp = 1.0f, recip_sqrt_spp = 1.0f;
+    int width = 0, height = 0;
+    int proc_rank = 0, proc_world = 1, stripe_rows = 16;
+    int n_dnodes = 0;
+    bool uv_always = false;
+    bool validated = false;
+    uint64_t last_ns = 0;
+};
+
+namespace {
+
+int set_err(rt_ctx* c, int code, const std::string& m) {
+    if (c) c->err = m;
+    return code;
+}
+
+#define HIPCHK(ctx, call)                                                                           \
+    do {                                                                                            \
+        hipError_t e_ = (call);                                                                     \
+        if (e_ != hipSuccess)                                                                       \
+            return set_err(ctx, RT_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+int dev_alloc_copy(rt_ctx* c, Device& d, DevBuf& b, const void* src, size_t n) {
+    HIPCHK(c, hipSetDevice(d.id));
+    if (b.ptr && b.bytes < n) {
+        HIPCHK(c, hipFree(b.ptr));
+        b.ptr = nullptr;
+        b.bytes = 0;
+    }
+    if (!b.ptr && n > 0) {
+        HIPCHK(c, hipMalloc(&b.ptr, n));
+        b.bytes = n;
+    }
+    if (n > 0) HIPCHK(c, hipMemcpy(b.ptr, src, n, hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+void dev_free(DevBuf& b) {
+    if (b.ptr) (void)hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.bytes = 0;
+}
+
+int local_rows_of(int h, int rank, int world, int stripe) {
+    if (h <= 0 || world <= 0 || stripe <= 0) return 0;
+    int n = 0;
+    int n_stripes = (h + stripe - 1) / stripe;
+    for (int s = rank; s < n_stripes; s += world) n += std::min(stripe, h - s * stripe);
+    return n;
+}
+
+int padded_rows_of(int h, int world, int stripe) {
+    int n_stripes = (h + stripe - 1) / stripe;
+    return ((n_stripes + world - 1) / world) * stripe;
+}
+
+// Re-lay the reference's pre-order BVH (BVHNode.java:13-56) as a threaded
+// array in the reference traversal's own visiting order (right child first).
+int thread_bvh(rt_ctx* c, const rt_bvh_node* in, int n, std::vector<rt_dnode>& out) {
+    out.clear();
+    if (n == 0) return RT_OK;
+    struct Item { int src; int depth; };
+    // Explicit DFS producing right-first pre-order; skip links patched after.
+    std::vector<int> order_src;
+    std::vector<int> skip_parent;   // for each emitted node: index of the emitted node whose skip it inherits (-1 = END)
+    struct Frame { int src; int inherit_skip_from_emitted; int left_sibling_src; int depth; };
+    // Iterative: emit node, then (if inner) process right subtree whose skip = first node of left subtree,
+    // then left subtree whose skip = this node's skip.
+    // We compute skip by a second pass: skip(node) = next emitted node after its subtree.
+    std::vector<int> subtree_end;   // emitted index one past this node's subtree
+    std::vector<int> stack_src, stack_depth, stack_emitted;
+    // recursive lambda with explicit stack to avoid deep recursion
+    struct Work { int src; int depth; int phase; int emitted; };
+    std::vector<Work> st;
+    st.push_back({0, 1, 0, -1});
+    const size_t kMaxNodes = (size_t)RT_MAX_RECORDS;
+    while (!st.empty()) {
+        Work& w = st.back();
+        if (w.phase == 0) {
+            if (w.src < 0 || w.src >= n) return set_err(c, RT_ERR_INVALID_ARG, "BVH child index out of range");
+            if (w.depth > RT_MAX_BVH_DEPTH) return set_err(c, RT_ERR_LIMIT, "BVH deeper than the reference's stack[64]");
+            if (order_src.size() >= kMaxNodes) return set_err(c, RT_ERR_LIMIT, "threaded BVH exceeds 65535 nodes");
+            w.emitted = (int)order_src.size();
+            order_src.push_back(w.src);
+            subtree_end.push_back(0);
+            const rt_bvh_node& nd = in[w.src];
+            int lt = nd.left_id & 0xFFFF;
+            if (lt != 0) {
+                subtree_end[w.emitted] = w.emitted + 1;
+                st.pop_back();
+                continue;
+            }
+            w.phase = 1;
+            int right = (nd.right_id >> 16) & 0xFFFF;
+            int depth = w.depth;
+            st.push_back({right, depth + 1, 0, -1});
+        } else if (w.phase == 1) {
+            w.phase = 2;
+            const rt_bvh_node& nd = in[w.src];
+            int left = (nd.left_id >> 16) & 0xFFFF;
+            int depth = w.depth;
+            st.push_back({left, depth + 1, 0, -1});
+        } else {
+            subtree_end[w.emitted] = (int)order_src.size();
+            st.pop_back();
+        }
+    }
+    int m = (int)order_src.size();
+    out.resize(m);
+    for (int k = 0; k < m; k++) {
+        const rt_bvh_node& nd = in[order_src[k]];
+        rt_dnode& d = out[k];
+        d.xmin = nd.xmin; d.xmax = nd.xmax; d.ymin = nd.ymin; d.ymax = nd.ymax; d.zmin = nd.zmin; d.zmax = nd.zmax;
+        int e = subtree_end[k];
+        uint32_t skip = (e >= m) ? RT_NODE_END : (uint32_t)e;
+        uint32_t lt = (uint32_t)(nd.left_id & 0xFFFF), rt = (uint32_t)(nd.right_id & 0xFFFF);
+        if (lt != 0) {
+            if (lt > 15 || rt > 15 || rt == 0) return set_err(c, RT_ERR_INVALID_ARG, "BVH leaf with bad model type");
+            d.meta = skip | (lt << 16) | (rt << 20);
+            d.prims = (uint32_t)((nd.left_id >> 16) & 0xFFFF) | ((uint32_t)((nd.right_id >> 16) & 0xFFFF) << 16);
+        } else {
+            d.meta = skip;
+            d.prims = 0;
+        }
+    }
+    return RT_OK;
+}
+
+int validate(rt_ctx* c) {
+    if (c->validated) return RT_OK;
+    size_t ns = c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere);
+    size_t nq = c->host_buf[RT_BIND_QUADS].size() / sizeof(rt_quad);
+    size_t nb = c->host_buf[RT_BIND_BOXES].size() / sizeof(rt_box);
+    size_t nm = c->host_buf[RT_BIND_MEDIA].size() / sizeof(rt_medium);
+    auto check_ref = [&](int type, int idx) -> bool {
+        switch (type) {
+            case RT_MODEL_SPHERE: return (size_t)idx < ns;
+            case RT_MODEL_QUAD: return (size_t)idx < nq;
+            case RT_MODEL_BOX: return (size_t)idx < nb;
+            case RT_MODEL_CONSTANT_MEDIUM: return (size_t)idx < nm;
+            default: return true;   // unknown types never hit (hit_model returns false)
+        }
+    };
+    const rt_bvh_node* nodes = (const rt_bvh_node*)c->host_buf[RT_BIND_BVH].data();
+    size_t nn = c->host_buf[RT_BIND_BVH].size() / sizeof(rt_bvh_node);
+    for (size_t i = 0; i < nn; i++) {
+        int lt = nodes[i].left_id & 0xFFFF;
+        if (lt == 0) continue;
+        if (!check_ref(lt, (nodes[i].left_id >> 16) & 0xFFFF) || !check_ref(nodes[i].right_id & 0xFFFF, (nodes[i].right_id >> 16) & 0xFFFF))
+            return set_err(c, RT_ERR_INVALID_ARG, "BVH leaf references a missing record");
+    }
+    const rt_medium* media = (const rt_medium*)c->host_buf[RT_BIND_MEDIA].data();
+    c->uv_always = false;
+    for (size_t i = 0; i < nm; i++) {
+        int bt = media[i].boundary_type;
+        if (bt == RT_MODEL_CONSTANT_MEDIUM) return set_err(c, RT_ERR_INVALID_ARG, "medium boundary cannot be a medium");
+        if (!check_ref(bt, media[i].boundary_idx) || media[i].boundary_idx < 0)
+            return set_err(c, RT_ERR_INVALID_ARG, "medium boundary references a missing record");
+        if (((media[i].texture_id >> 28) & 0xF) == RT_TEXTYPE_IMAGE) c->uv_always = true;
+    }
+    const std::vector<uint8_t>& L = c->host_buf[RT_BIND_LIGHTS];
+    if (L.size() >= 4) {
+        int32_t count;
+        std::memcpy(&count, L.data(), 4);
+        if (count < 0 || (size_t)(count + 1) * 4 > L.size()) return set_err(c, RT_ERR_INVALID_ARG, "lights count exceeds buffer");
+        for (int i = 0; i < count; i++) {
+            int32_t p;
+            std::memcpy(&p, L.data() + 4 + 4 * i, 4);
+            int t = (p >> 16) & 0xFFFF, ix = p & 0xFFFF;
+            if ((t == RT_MODEL_SPHERE || t == RT_MODEL_QUAD) && !check_ref(t, ix))
+                return set_err(c, RT_ERR_INVALID_ARG, "light references a missing record");
+        }
+    }
+    c->validated = true;
+    return RT_OK;
+}
+
+int alloc_image(rt_ctx* c, Device& d) {
+    HIPCHK(c, hipSetDevice(d.id));
+    d.local_rows = local_rows_of(c->height, d.rank, d.world, c->stripe_rows);
+    d.padded_rows = padded_rows_of(c->height, d.world, c->stripe_rows);
+    size_t bytes = (size_t)d.padded_rows * c->width * 16;
+    dev_free(d.image);
+    if (bytes) {
+        HIPCHK(c, hipMalloc(&d.image.ptr, bytes));
+        d.image.bytes = bytes;
+        HIPCHK(c, hipMemset(d.image.ptr, 0, bytes));
+    }
+    d.image_ptr = (float*)d.image.ptr;
+    d.image_bound = false;
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
+    if (!out) return RT_ERR_INVALID_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RT_ERR_DEVICE;
+    if (n_devices <= 0 || n_devices > count) return RT_ERR_INVALID_ARG;
+    rt_ctx* c = new rt_ctx();
+    c->devs.resize(n_devices);
+    for (int i = 0; i < n_devices; i++) {
+        Device& d = c->devs[i];
+        d.id = device_ids ? device_ids[i] : i;
+        if (d.id < 0 || d.id >= count) { delete c; return RT_ERR_INVALID_ARG; }
+        d.rank = i;
+        d.world = n_devices;
+        if (hipSetDevice(d.id) != hipSuccess || hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreate(&d.ev_start) != hipSuccess || hipEventCreate(&d.ev_stop) != hipSuccess) {
+            delete c;
+            return RT_ERR_DEVICE;
+        }
+    }
+    *out = c;
+    return RT_OK;
+}
+
+int rt_destroy(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    for (Device& d : c->devs) {
+        (void)hipSetDevice(d.id);
+        (void)hipStreamSynchronize(d.stream);
+        dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
+        dev_free(d.lights); dev_free(d.image); dev_free(d.args);
+        for (auto& t : d.tex) dev_free(t);
+        if (d.ev_start) (void)hipEventDestroy(d.ev_start);
+        if (d.ev_stop) (void)hipEventDestroy(d.ev_stop);
+        if (d.own_stream && d.stream) (void)hipStreamDestroy(d.stream);
+    }
+    delete c;
+    return RT_OK;
+}
+
+const char* rt_last_error(rt_ctx* c) { return c ? c->err.c_str() : "NULL context"; }
+
+int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (binding < 0 || binding > 5) return set_err(c, RT_ERR_INVALID_ARG, "binding must be 0..5");
+    if (nbytes && !bytes) return set_err(c, RT_ERR_INVALID_ARG, "NULL bytes");
+    static const size_t rec[6] = {sizeof(rt_sphere), sizeof(rt_bvh_node), sizeof(rt_quad), sizeof(rt_medium),
+                                  sizeof(rt_box), 4};
+    if (nbytes % rec[binding]) return set_err(c, RT_ERR_INVALID_ARG, "size is not a multiple of the std430 record size");
+    if (binding != RT_BIND_LIGHTS && nbytes / rec[binding] > RT_MAX_RECORDS)
+        return set_err(c, RT_ERR_LIMIT, "more than 65535 records");
+    std::vector<uint8_t>& H = c->host_buf[binding];
+    H.assign((const uint8_t*)bytes, (const uint8_t*)bytes + nbytes);
+    c->uploaded[binding] = true;
+    c->validated = false;
+    std::vector<uint8_t> dev_bytes;
+    const void* src = bytes;
+    size_t n = nbytes;
+    if (binding == RT_BIND_BVH) {
+        std::vector<rt_dnode> dn;
+        int r = thread_bvh(c, (const rt_bvh_node*)H.data(), (int)(nbytes / sizeof(rt_bvh_node)), dn);
+        if (r) return r;
+        c->n_dnodes = (int)dn.size();
+        dev_bytes.assign((uint8_t*)dn.data(), (uint8_t*)dn.data() + dn.size() * sizeof(rt_dnode));
+        src = dev_bytes.data();
+        n = dev_bytes.size();
+    }
+    if (binding == RT_BIND_LIGHTS) {
+        if (nbytes < 4) return set_err(c, RT_ERR_INVALID_ARG, "lights buffer needs the count word");
+        src = (const uint8_t*)bytes + 4;
+        n = nbytes - 4;
+    }
+    for (Device& d : c->devs) {
+        DevBuf* b = nullptr;
+        switch (binding) {
+            case RT_BIND_SPHERES: b = &d.spheres; break;
+            case RT_BIND_BVH: b = &d.nodes; break;
+            case RT_BIND_QUADS: b = &d.quads; break;
+            case RT_BIND_MEDIA: b = &d.media; break;
+            case RT_BIND_BOXES: b = &d.boxes; break;
+            default: b = &d.lights; break;
+        }
+        int r = dev_alloc_copy(c, d, *b, src, n);
+        if (r) return r;
+    }
+    return RT_OK;
+}
+
+int rt_upload_texture(rt_ctx* c, int slot, int format, int w, int h, const void* texels) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (slot < 0 || slot >= RT_MAX_TEXTURES) return set_err(c, RT_ERR_LIMIT, "texture slot must be 0..7");
+    if (w <= 0 || h <= 0 || !texels) return set_err(c, RT_ERR_INVALID_ARG, "bad texture size or NULL texels");
+    if ((size_t)w * h > (size_t)1 << 28) return set_err(c, RT_ERR_LIMIT, "texture too large");
+    size_t n = (size_t)w * h;
+    std::vector<uint32_t> rgba;
+    const void* src = texels;
+    size_t bytes = n * 4;
+    if (format == RT_TEX_RGB8) {
+        rgba.resize(n);
+        const uint8_t* p = (const uint8_t*)texels;
+        for (size_t i = 0; i < n; i++)
+            rgba[i] = (uint32_t)p[3 * i] | ((uint32_t)p[3 * i + 1] << 8) | ((uint32_t)p[3 * i + 2] << 16) | 0xFF000000u;
+        src = rgba.data();
+    } else if (format != RT_TEX_RGBA8 && format != RT_TEX_R32F) {
+        return set_err(c, RT_ERR_INVALID_ARG, "unknown texture format");
+    }
+    for (Device& d : c->devs) {
+        int r = dev_alloc_copy(c, d, d.tex[slot], src, bytes);
+        if (r) return r;
+    }
+    c->tex_format[slot] = format;
+    c->tex_w[slot] = w;
+    c->tex_h[slot] = h;
+    return RT_OK;
+}
+
+int rt_set_camera(rt_ctx* c, const float ubo[28]) {
+    if (!c || !ubo) return set_err(c, RT_ERR_INVALID_ARG, "NULL camera");
+    std::memcpy(&c->cam, ubo, sizeof(rt_camera_ubo));
+    c->have_cam = true;
+    return RT_OK;
+}
+
+int rt_set_params(rt_ctx* c, int max_depth, const float background[3], float sqrt_spp, float recip_sqrt_spp) {
+    if (!c || !background) return set_err(c, RT_ERR_INVALID_ARG, "NULL background");
+    if (max_depth < 0) return set_err(c, RT_ERR_INVALID_ARG, "max_depth must be >= 0");
+    c->max_depth = max_depth;
+    std::memcpy(c->background, background, 12);
+    c->sqrt_spp = sqrt_spp;
+    c->recip_sqrt_spp = recip_sqrt_spp;
+    return RT_OK;
+}
+
+int rt_set_partition(rt_ctx* c, int rank, int world, int stripe_rows) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (world < 1 || rank < 0 || rank >= world || stripe_rows < 1) return set_err(c, RT_ERR_INVALID_ARG, "bad partition");
+    if (world > 1 && c->devs.size() != 1) return set_err(c, RT_ERR_STATE, "process partition needs a 1-device context");
+    c->proc_rank = rank;
+    c->proc_world = world;
+    c->stripe_rows = stripe_rows;
+    if (c->devs.size() == 1) {
+        c->devs[0].rank = rank;
+        c->devs[0].world = world;
+    }
+    if (c->width > 0) return rt_resize(c, c->width, c->height);
+    return RT_OK;
+}
+
+int rt_local_rows(int height, int rank, int world, int stripe_rows) { return local_rows_of(height, rank, world, stripe_rows); }
+int rt_padded_local_rows(int height, int world, int stripe_rows) {
+    if (height <= 0 || world <= 0 || stripe_rows <= 0) return 0;
+    return padded_rows_of(height, world, stripe_rows);
+}
+
+int rt_resize(rt_ctx* c, int w, int h) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (w <= 0 || h <= 0 || (size_t)w * h > ((size_t)1 << 30)) return set_err(c, RT_ERR_INVALID_ARG, "bad image size");
+    c->width = w;
+    c->height = h;
+    for (Device& d : c->devs) {
+        int r = alloc_image(c, d);
+        if (r) return r;
+    }
+    return RT_OK;
+}
+
+int rt_bind_device_image(rt_ctx* c, void* ptr, size_t nbytes) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (c->devs.size() != 1) return set_err(c, RT_ERR_STATE, "device image binding needs a 1-device context");
+    Device& d = c->devs[0];
+    if (c->width <= 0) return set_err(c, RT_ERR_STATE, "rt_resize first");
+    if (!ptr) {
+        d.image_ptr = (float*)d.image.ptr;
+        d.image_bound = false;
+        return RT_OK;
+    }
+    if (nbytes < (size_t)d.padded_rows * c->width * 16) return set_err(c, RT_ERR_INVALID_ARG, "device image too small");
+    d.image_ptr = (float*)ptr;
+    d.image_bound = true;
+    return RT_OK;
+}
+
+int rt_set_stream(rt_ctx* c, void* stream) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (c->devs.size() != 1) return set_err(c, RT_ERR_STATE, "stream binding needs a 1-device context");
+    Device& d = c->devs[0];
+    HIPCHK(c, hipSetDevice(d.id));
+    if (d.own_stream && d.stream) HIPCHK(c, hipStreamSynchronize(d.stream));
+    if (!stream) {
+        if (!d.own_stream) {
+            HIPCHK(c, hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+            d.own_stream = true;
+        }
+        return RT_OK;
+    }
+    if (d.own_stream && d.stream) HIPCHK(c, hipStreamDestroy(d.stream));
+    d.stream = (hipStream_t)stream;
+    d.own_stream = false;
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factors) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (first_frame < 1 || n_frames < 0 || (n_frames > 0 && !rand_factors))
+        return set_err(c, RT_ERR_INVALID_ARG, "first_frame >= 1, n_frames >= 0, rand_factors required");
+    if (c->width <= 0) return set_err(c, RT_ERR_STATE, "rt_resize before rt_render");
+    if (!c->have_cam) return set_err(c, RT_ERR_STATE, "rt_set_camera before rt_render");
+    if (!c->uploaded[RT_BIND_BVH]) return set_err(c, RT_ERR_STATE, "no BVH uploaded");
+    int r = validate(c);
+    if (r) return r;
+    rt_kernel_args a;
+    std::memset(&a, 0, sizeof(a));
+    a.n_nodes = c->n_dnodes;
+    int32_t lc = 0;
+    if (c->host_buf[RT_BIND_LIGHTS].size() >= 4) std::memcpy(&lc, c->host_buf[RT_BIND_LIGHTS].data(), 4);
+    a.lights_count = lc;
+    a.uv_always = c->uv_always;
+    a.cam = c->cam;
+    std::memcpy(a.background, c->background, 12);
+    a.max_depth = c->max_depth;
+    a.sqrt_spp = c->sqrt_spp;
+    a.recip_sqrt_spp = c->recip_sqrt_spp;
+    a.width = c->width;
+    a.height = c->height;
+    a.stripe_rows = c->stripe_rows;
+    uint64_t max_ns = 0;
+    for (Device& d : c->devs) {
+        HIPCHK(c, hipSetDevice(d.id));
+        a.nodes = (const rt_dnode*)d.nodes.ptr;
+        a.spheres = (const rt_sphere*)d.spheres.ptr;
+        a.quads = (const rt_quad*)d.quads.ptr;
+        a.boxes = (const rt_box*)d.boxes.ptr;
+        a.media = (const rt_medium*)d.media.ptr;
+        a.lights = (const int32_t*)d.lights.ptr;
+        for (int t = 0; t < 8; t++) {
+            a.tex[t].data = d.tex[t].ptr;
+            a.tex[t].w = c->tex_w[t];
+            a.tex[t].h = c->tex_h[t];
+            a.tex[t].is_float = c->tex_format[t] == RT_TEX_R32F;
+        }
+        a.image = d.image_ptr;
+        a.local_rows = d.local_rows;
+        a.rank = d.rank;
+        a.world = d.world;
+        if (!d.args.ptr) {
+            HIPCHK(c, hipMalloc(&d.args.ptr, sizeof(rt_kernel_args)));
+            d.args.bytes = sizeof(rt_kernel_args);
+        }
+        HIPCHK(c, hipEventRecord(d.ev_start, d.stream));
+        for (int f0 = 0; f0 < n_frames; f0 += RT_MAX_FRAMES_PER_LAUNCH) {
+            int nf = std::min(RT_MAX_FRAMES_PER_LAUNCH, n_frames - f0);
+            a.first_frame = first_frame + f0;
+            a.n_frames = nf;
+            std::memcpy(a.rand_factors, rand_factors + f0, sizeof(float) * nf);
+            if (rt_launch_render(a, (rt_kernel_args*)d.args.ptr, d.stream))
+                return set_err(c, RT_ERR_DEVICE, "kernel launch failed");
+        }
+        HIPCHK(c, hipEventRecord(d.ev_stop, d.stream));
+        d.timed = true;
+    }
+    (void)max_ns;
+    return RT_OK;
+}
+
+int rt_sync(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    for (Device& d : c->devs) {
+        HIPCHK(c, hipSetDevice(d.id));
+        HIPCHK(c, hipStreamSynchronize(d.stream));
+    }
+    return RT_OK;
+}
+
+int rt_last_render_ns(rt_ctx* c, uint64_t* ns) {
+    if (!c || !ns) return RT_ERR_INVALID_ARG;
+    double mx = 0;
+    for (Device& d : c->devs) {
+        if (!d.timed) continue;
+        HIPCHK(c, hipSetDevice(d.id));
+        HIPCHK(c, hipEventSynchronize(d.ev_stop));
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, d.ev_start, d.ev_stop));
+        mx = std::max(mx, (double)ms);
+    }
+    *ns = (uint64_t)(mx * 1e6);
+    c->last_ns = *ns;
+    return RT_OK;
+}
+
+int rt_read_image(rt_ctx* c, float* rgba) {
+    if (!c || !rgba) return RT_ERR_INVALID_ARG;
+    if (c->width <= 0) return set_err(c, RT_ERR_STATE, "no image");
+    int r = rt_sync(c);
+    if (r) return r;
+    if (c->devs.size() == 1) {
+        Device& d = c->devs[0];
+        HIPCHK(c, hipSetDevice(d.id));
+        HIPCHK(c, hipMemcpy(rgba, d.image_ptr, (size_t)d.local_rows * c->width * 16, hipMemcpyDeviceToHost));
+        return RT_OK;
+    }
+    // multi-device context: gather stripes to the host and de-interleave
+    int ndev = (int)c->devs.size();
+    int padded = padded_rows_of(c->height, ndev, c->stripe_rows);
+    std::vector<float> g((size_t)ndev * padded * c->width * 4, 0.0f);
+    for (int k = 0; k < ndev; k++) {
+        Device& d = c->devs[k];
+        HIPCHK(c, hipSetDevice(d.id));
+        HIPCHK(c, hipMemcpy(g.data() + (size_t)k * padded * c->width * 4, d.image_ptr,
+                            (size_t)d.local_rows * c->width * 16, hipMemcpyDeviceToHost));
+    }
+    return rt_deinterleave_rows(g.data(), c->width, c->height, ndev, c->stripe_rows, rgba);
+}
+
+int rt_write_image(rt_ctx* c, const float* rgba) {
+    if (!c || !rgba) return RT_ERR_INVALID_ARG;
+    if (c->width <= 0) return set_err(c, RT_ERR_STATE, "no image");
+    int r = rt_sync(c);
+    if (r) return r;
+    for (Device& d : c->devs) {
+        HIPCHK(c, hipSetDevice(d.id));
+        std::vector<float> local((size_t)d.local_rows * c->width * 4);
+        // pick this device's rows from the (process-local) image
+        if (c->devs.size() == 1) {
+            HIPCHK(c, hipMemcpy(d.image_ptr, rgba, local.size() * 4, hipMemcpyHostToDevice));
+            continue;
+        }
+        int n_stripes = (c->height + c->stripe_rows - 1) / c->stripe_rows;
+        size_t lr = 0;
+        for (int s = d.rank; s < n_stripes; s += d.world)
+            for (int y = s * c->stripe_rows; y < std::min(c->height, (s + 1) * c->stripe_rows); y++, lr++)
+                std::memcpy(&local[lr * c->width * 4], rgba + (size_t)y * c->width * 4, (size_t)c->width * 16);
+        HIPCHK(c, hipMemcpy(d.image_ptr, local.data(), local.size() * 4, hipMemcpyHostToDevice));
+    }
+    return RT_OK;
+}
+
+int rt_deinterleave_rows(const float* gathered, int width, int height, int world, int stripe_rows, float* out) {
+    if (!gathered || !out || width <= 0 || height <= 0 || world < 1 || stripe_rows < 1) return RT_ERR_INVALID_ARG;
+    int padded = padded_rows_of(height, world, stripe_rows);
+    int n_stripes = (height + stripe_rows - 1) / stripe_rows;
+    for (int k = 0; k < world; k++) {
+        size_t lr = 0;
+        for (int s = k; s < n_stripes; s += world)
+            for (int y = s * stripe_rows; y < std::min(height, (s + 1) * stripe_rows); y++, lr++)
+                std::memcpy(out + (size_t)y * width * 4, gathered + ((size_t)k * padded + lr) * width * 4,
+                            (size_t)width * 16);
+    }
+    return RT_OK;
+}
+
+float rt_frame_rand_factor(uint64_t seed, uint64_t frame_index) {
+    uint64_t z = seed + (frame_index + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return (float)(uint32_t)(z >> 40) / 16777216.0f;
+}
+
+// ---- debug / test hooks (rt_debug.h)
+int rt_debug_eval_builtin(int device, int fn, const float* x, const float* y, float* out, int n) {
+    if (!x || !out || n < 0) return RT_ERR_INVALID_ARG;
+    if (n == 0) return RT_OK;
+    if (hipSetDevice(device) != hipSuccess) return RT_ERR_DEVICE;
+    float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    size_t b = (size_t)n * 4;
+    int rc = RT_OK;
+    if (hipMalloc(&dx, b) != hipSuccess || hipMalloc(&dout, b) != hipSuccess || (y && hipMalloc(&dy, b) != hipSuccess))
+        rc = RT_ERR_DEVICE;
+    if (!rc && hipMemcpy(dx, x, b, hipMemcpyHostToDevice) != hipSuccess) rc = RT_ERR_DEVICE;
+    if (!rc && y && hipMemcpy(dy, y, b, hipMemcpyHostToDevice) != hipSuccess) rc = RT_ERR_DEVICE;
+    if (!rc && rt_launch_eval_builtin(fn, dx, dy, dout, n, nullptr)) rc = RT_ERR_DEVICE;
+    if (!rc && hipMemcpy(out, dout, b, hipMemcpyDeviceToHost) != hipSuccess) rc = RT_ERR_DEVICE;
+    if (dx) (void)hipFree(dx);
+    if (dy) (void)hipFree(dy);
+    if (dout) (void)hipFree(dout);
+    return rc;
+}
+
+int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t out_cap, int* n_out) {
+    if (!nodes || !n_out || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
+    std::vector<rt_dnode> dn;
+    rt_ctx tmp;
+    int r = thread_bvh(&tmp, (const rt_bvh_node*)nodes, (int)(nbytes / sizeof(rt_bvh_node)), dn);
+    if (r) return r;
+    *n_out = (int)dn.size();
+    if (out) {
+        if (out_cap < dn.size() * sizeof(rt_dnode)) return RT_ERR_INVALID_ARG;
+        std::memcpy(out, dn.data(), dn.size() * sizeof(rt_dnode));
+    }
+    return RT_OK;
+}
+
+int rt_debug_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,69 @@
+// rt_device.h — device-side scene layout and kernel arguments (internal to
+// librtamd.so; not part of the C ABI).
+//
+// HBM layout per device (all replicated on every device):
+//   nodes    : threaded BVH, right-first pre-order (see rt_bvh_thread.cpp), 32 B/node
+//   spheres  : rt_sphere[] as uploaded (48 B AoS)
+//   quads    : rt_quad[]   as uploaded (80 B AoS)
+//   boxes    : rt_box[]    as uploaded (480 B AoS)
+//   media    : rt_medium[] as uploaded (20 B)
+//   lights   : int32 packed ids
+//   textures : RGB8 expanded to RGBA8 (4 B/texel, aligned), RGBA8, R32F
+//   image    : float4 [padded_local_rows][W], stripe-compacted rows
+#pragma once
+
+#include <stdint.h>
+
+#include "rt/rt_types.h"
+
+#define RT_MAX_FRAMES_PER_LAUNCH 256
+#define RT_NODE_END 0xFFFFu
+
+// Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
+// continues at index+1 (its RIGHT child, which the reference visits first
+// because it pushes left then right, compute.glsl:259-260); a leaf tests its
+// two prims (left then right, compute.glsl:247-256) and continues at `skip`;
+// on a miss continue at `skip`.  skip == RT_NODE_END ends the walk.  This
+// visits exactly the node sequence of the reference's int stack[64] walk.
+struct rt_dnode {
+    float xmin, xmax, ymin, ymax, zmin, zmax;
+    uint32_t meta;    // bits 0-15 skip, 16-19 left type (0 = inner node), 20-23 right type
+    uint32_t prims;   // bits 0-15 left index, 16-31 right index
+};
+static_assert(sizeof(rt_dnode) == 32, "device node is 32 B");
+
+struct rt_dtex {
+    const void* data;   // RGBA8 (uint32) or R32F
+    int w, h;
+    int is_float;       // 1 = R32F
+    int pad;
+};
+
+struct rt_kernel_args {
+    const rt_dnode* nodes;
+    const rt_sphere* spheres;
+    const rt_quad* quads;
+    const rt_box* boxes;
+    const rt_medium* media;
+    const int32_t* lights;
+    int n_nodes, lights_count;
+    int uv_always;       // a medium samples an image texture: keep sphere uv current (Q9)
+    int pad0;
+    rt_dtex tex[8];
+    rt_camera_ubo cam;
+    float background[3];
+    int max_depth;
+    float sqrt_spp, recip_sqrt_spp;
+    // image / partition
+    float* image;        // float4 rows, local-compact
+    int width, height;
+    int local_rows;
+    int rank, world, stripe_rows;
+    int first_frame, n_frames;
+    float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
+};
+
+// launcher implemented in rt_kernel.hip
+int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream);
+// debug: evaluate GLSL built-ins on device (tests)
+int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream);

@@ -1,0 +1,112 @@
+"""ctypes loaders for the two in-tree native libraries.
+
+* ``librtamd.so``   — the HIP kernel behind the C ABI of include/rt/rt.h.
+* ``librtscene.so`` — the host scene builder of include/rt/rt_scene.h.
+
+Both are built in-tree by ``make -C raytracing-book_amd`` (see
+__graft_entry__.build()).  There is no Python or CPU fallback for the render
+path: if librtamd.so is missing, loading raises.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+ASSET_DIR = os.path.join(REPO_DIR, "assets")
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+c_int_p = ctypes.POINTER(ctypes.c_int)
+
+_amd = None
+_scene = None
+
+
+class RTError(RuntimeError):
+    """A negative status from the C ABI, with rt_last_error()'s message."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"rt error {code}: {msg}")
+        self.code = code
+
+
+def _load(name):
+    path = os.path.join(LIB_DIR, name)
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build it with `make -C {PKG_DIR}` "
+            "(or __graft_entry__.build()); there is no fallback path")
+    return ctypes.CDLL(path)
+
+
+def _proto(lib, name, restype, *argtypes):
+    fn = getattr(lib, name)
+    fn.restype = restype
+    fn.argtypes = list(argtypes)
+    return fn
+
+
+class RtsInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "scene_id", "width", "height", "n_spheres", "n_quads", "n_boxes", "n_media",
+        "n_lights", "n_bvh_nodes", "n_bvh_prims", "bvh_depth", "max_stack", "n_textures")] + [
+        ("background", ctypes.c_float * 3)]
+
+
+def amd():
+    """The product library (HIP).  Raises ImportError when it was not built."""
+    global _amd
+    if _amd is None:
+        L = _load("librtamd.so")
+        vp, sz, i, f, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float, ctypes.c_uint64
+        _proto(L, "rt_abi_version", i)
+        _proto(L, "rt_create", i, i, c_int_p, ctypes.POINTER(vp))
+        _proto(L, "rt_destroy", i, vp)
+        _proto(L, "rt_last_error", ctypes.c_char_p, vp)
+        _proto(L, "rt_upload_buffer", i, vp, i, vp, sz)
+        _proto(L, "rt_upload_texture", i, vp, i, i, i, i, vp)
+        _proto(L, "rt_set_camera", i, vp, c_float_p)
+        _proto(L, "rt_set_params", i, vp, i, c_float_p, f, f)
+        _proto(L, "rt_resize", i, vp, i, i)
+        _proto(L, "rt_render", i, vp, i, i, c_float_p)
+        _proto(L, "rt_sync", i, vp)
+        _proto(L, "rt_read_image", i, vp, c_float_p)
+        _proto(L, "rt_write_image", i, vp, c_float_p)
+        _proto(L, "rt_last_render_ns", i, vp, ctypes.POINTER(u64))
+        _proto(L, "rt_set_partition", i, vp, i, i, i)
+        _proto(L, "rt_local_rows", i, i, i, i, i)
+        _proto(L, "rt_padded_local_rows", i, i, i, i)
+        _proto(L, "rt_bind_device_image", i, vp, vp, sz)
+        _proto(L, "rt_set_stream", i, vp, vp)
+        _proto(L, "rt_deinterleave_rows", i, c_float_p, i, i, i, i, c_float_p)
+        _proto(L, "rt_frame_rand_factor", f, u64, u64)
+        _proto(L, "rt_debug_eval_builtin", i, i, i, c_float_p, c_float_p, c_float_p, i)
+        _proto(L, "rt_debug_threaded_bvh", i, vp, sz, vp, sz, c_int_p)
+        _proto(L, "rt_debug_device_count", i)
+        _amd = L
+    return _amd
+
+
+def scene_lib():
+    """The host scene builder (no GPU needed)."""
+    global _scene
+    if _scene is None:
+        L = _load("librtscene.so")
+        vp, sz, i, f = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float
+        _proto(L, "rts_build", i, i, i, i, ctypes.c_uint64, ctypes.c_char_p, ctypes.POINTER(vp))
+        _proto(L, "rts_free", None, vp)
+        _proto(L, "rts_last_error", ctypes.c_char_p)
+        _proto(L, "rts_get_info", i, vp, ctypes.POINTER(RtsInfo))
+        _proto(L, "rts_get_buffer", i, vp, i, ctypes.POINTER(vp), ctypes.POINTER(sz))
+        _proto(L, "rts_get_texture", i, vp, i, c_int_p, c_int_p, c_int_p, ctypes.POINTER(vp), ctypes.POINTER(sz))
+        _proto(L, "rts_get_camera", i, vp, c_float_p)
+        _proto(L, "rts_set_image_size", i, vp, i, i)
+        _proto(L, "rts_spp_uniforms", None, i, c_float_p, c_float_p)
+        _proto(L, "rts_tonemap_rgb8", i, c_float_p, i, i, ctypes.POINTER(ctypes.c_uint8))
+        _proto(L, "rts_save_png", i, c_float_p, i, i, ctypes.c_char_p)
+        _proto(L, "rts_java_random_next_int", ctypes.c_int32, ctypes.c_int64, i)
+        _proto(L, "rts_java_random_next_double", ctypes.c_double, ctypes.c_int64, i)
+        _proto(L, "rts_java_random_next_float", f, ctypes.c_int64, i)
+        _proto(L, "rts_java_random_next_int_bound", ctypes.c_int32, ctypes.c_int64, i)
+        _scene = L
+    return _scene

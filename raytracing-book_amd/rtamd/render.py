@@ -1,0 +1,232 @@
+"""Render context and the RaytraceExecutor mirror over the rt.h C ABI.
+
+``RenderContext`` owns an ``rt_ctx`` (one or more MI355X devices, or one
+stripe-partition of a multi-process render) and uploads a ``Scene`` the way the
+reference's Java side fills its SSBOs/UBO/textures.  ``RaytraceExecutor``
+restates J/system/RaytraceExecutor.java (setSamplePerPixel, raytrace,
+sampleComplete, resetCompleteState, completion listeners) with frames batched
+per kernel launch instead of one dispatch per vsync.
+"""
+import ctypes
+import time
+
+import numpy as np
+
+from . import _lib
+from ._lib import RTError, c_float_p
+from .scene import Scene, spp_uniforms
+
+MASK64 = (1 << 64) - 1
+
+
+def frame_rand_factors(seed, start, n):
+    """u_rand_factor for frames [start, start+n): top 24 bits of
+    splitmix64(seed, frame)/2^24 (rt.h rt_frame_rand_factor; stands in for the
+    reference's per-frame (float)Math.random(), RaytraceExecutor.java:124)."""
+    out = np.empty(n, dtype=np.float32)
+    for k in range(n):
+        z = (seed + (start + k + 1) * 0x9E3779B97F4A7C15) & MASK64
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+        z ^= z >> 31
+        out[k] = np.float32(z >> 40) / np.float32(16777216.0)
+    return out
+
+
+def local_rows(height, rank, world, stripe_rows):
+    n_stripes = (height + stripe_rows - 1) // stripe_rows
+    return sum(min(stripe_rows, height - s * stripe_rows) for s in range(rank, n_stripes, world))
+
+
+def padded_local_rows(height, world, stripe_rows):
+    n_stripes = (height + stripe_rows - 1) // stripe_rows
+    return ((n_stripes + world - 1) // world) * stripe_rows
+
+
+def stripe_rows_of(height, rank, world, stripe_rows):
+    """Global row indices owned by `rank`, in local (compact) order."""
+    n_stripes = (height + stripe_rows - 1) // stripe_rows
+    rows = []
+    for s in range(rank, n_stripes, world):
+        rows.extend(range(s * stripe_rows, min(height, (s + 1) * stripe_rows)))
+    return np.array(rows, dtype=np.int64)
+
+
+def deinterleave(gathered, height, world, stripe_rows):
+    """[world, padded_rows, W, 4] gathered stripe blocks -> [H, W, 4] image."""
+    W = gathered.shape[2]
+    out = np.zeros((height, W, 4), dtype=gathered.dtype)
+    for k in range(world):
+        rows = stripe_rows_of(height, k, world, stripe_rows)
+        out[rows] = gathered[k, :len(rows)]
+    return out
+
+
+class RenderContext:
+    """An rt_ctx: device buffers, accumulation image and launch state."""
+
+    def __init__(self, devices=(0,), rank=0, world=1, stripe_rows=16):
+        L = _lib.amd()
+        self._L = L
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        rc = L.rt_create(len(devices), devs, ctypes.byref(h))
+        if rc != 0:
+            raise RTError(rc, "rt_create failed (no HIP device visible?)")
+        self._h = h
+        self.devices = tuple(devices)
+        self.rank, self.world, self.stripe_rows = rank, world, stripe_rows
+        if world > 1 or stripe_rows != 16:
+            self._check(L.rt_set_partition(h, rank, world, stripe_rows))
+        self.width = self.height = 0
+        self.max_depth = 5
+        self.background = np.zeros(3, np.float32)
+        self.sqrt_spp, self.recip_sqrt_spp = 1.0, 1.0
+
+    def _check(self, rc):
+        if rc != 0:
+            raise RTError(rc, self._L.rt_last_error(self._h).decode())
+        return rc
+
+    # -- scene upload (RaytraceModel.putModelsToProgram, Texture.putData, Camera.init)
+    def upload_scene(self, scene: Scene):
+        for b in range(6):
+            data = scene.buffers[b]
+            buf = ctypes.create_string_buffer(data, len(data)) if data else None
+            self._check(self._L.rt_upload_buffer(self._h, b, buf, len(data)))
+        for t in scene.textures:
+            buf = ctypes.create_string_buffer(t.data, len(t.data))
+            self._check(self._L.rt_upload_texture(self._h, t.slot, t.format, t.width, t.height, buf))
+        self.set_camera(scene.camera)
+        self.background = scene.background.copy()
+
+    def set_camera(self, ubo):
+        ubo = np.ascontiguousarray(ubo, dtype=np.float32)
+        assert ubo.size == 28
+        self._check(self._L.rt_set_camera(self._h, ubo.ctypes.data_as(c_float_p)))
+
+    def set_params(self, max_depth=None, background=None, spp=None):
+        if max_depth is not None:
+            self.max_depth = int(max_depth)
+        if background is not None:
+            self.background = np.asarray(background, np.float32)
+        if spp is not None:
+            self.sqrt_spp, self.recip_sqrt_spp = spp_uniforms(spp)
+        bg = np.ascontiguousarray(self.background, dtype=np.float32)
+        self._check(self._L.rt_set_params(self._h, self.max_depth, bg.ctypes.data_as(c_float_p),
+                                          self.sqrt_spp, self.recip_sqrt_spp))
+
+    def resize(self, width, height):
+        self._check(self._L.rt_resize(self._h, int(width), int(height)))
+        self.width, self.height = int(width), int(height)
+
+    @property
+    def local_rows(self):
+        if len(self.devices) > 1:
+            return self.height
+        return local_rows(self.height, self.rank, self.world, self.stripe_rows)
+
+    @property
+    def padded_rows(self):
+        return padded_local_rows(self.height, self.world, self.stripe_rows)
+
+    def render(self, first_frame, rand_factors):
+        rf = np.ascontiguousarray(rand_factors, dtype=np.float32)
+        self._check(self._L.rt_render(self._h, int(first_frame), int(rf.size), rf.ctypes.data_as(c_float_p)))
+
+    def sync(self):
+        self._check(self._L.rt_sync(self._h))
+
+    def last_render_ns(self):
+        v = ctypes.c_uint64()
+        self._check(self._L.rt_last_render_ns(self._h, ctypes.byref(v)))
+        return v.value
+
+    def read_image(self):
+        """[local_rows, W, 4] float32 (the full image for an unpartitioned context)."""
+        out = np.empty((self.local_rows, self.width, 4), dtype=np.float32)
+        self._check(self._L.rt_read_image(self._h, out.ctypes.data_as(c_float_p)))
+        return out
+
+    def write_image(self, rgba):
+        rgba = np.ascontiguousarray(rgba, dtype=np.float32)
+        self._check(self._L.rt_write_image(self._h, rgba.ctypes.data_as(c_float_p)))
+
+    def bind_device_image(self, ptr, nbytes):
+        self._check(self._L.rt_bind_device_image(self._h, ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes)))
+
+    def set_stream(self, stream_ptr):
+        self._check(self._L.rt_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RaytraceExecutor:
+    """J/system/RaytraceExecutor.java over an rt_ctx.
+
+    One reference ``raytrace()`` = one dispatch = one frame (1 spp) per vsync;
+    here ``raytrace(n)`` queues n frames in one rt_render call, with the same
+    per-frame uniforms (frame_count = ++numSamples, u_rand_factor).
+    """
+
+    def __init__(self, ctx: RenderContext, seed=1):
+        self.ctx = ctx
+        self.seed = seed
+        self._listeners = []
+        self.samplePerPixel = 0
+        self.resetCompleteState()
+        self.lastDispatchTime = 0
+
+    def setSamplePerPixel(self, spp):            # :50-56
+        self.samplePerPixel = int(spp)
+        self.ctx.set_params(spp=spp)
+
+    def resetCompleteState(self):                # :58-62
+        self.isSampleComplete = False
+        self.numSamples = 0
+        self.finishTime = -1
+
+    def getNumSamples(self):
+        return self.numSamples
+
+    def getSamplePerPixel(self):
+        return self.samplePerPixel
+
+    def getFinishTime(self):
+        return self.finishTime
+
+    def getLastDispatchTime(self):
+        return self.lastDispatchTime
+
+    def addCompleteListener(self, fn):           # :96-98
+        self._listeners.append(fn)
+
+    def raytrace(self, n_frames=1):              # :100-142
+        if self.numSamples == 0:
+            self._start = time.time()
+        n = max(0, min(int(n_frames), self.samplePerPixel - self.numSamples)) if self.samplePerPixel else int(n_frames)
+        if n == 0:
+            return
+        rf = frame_rand_factors(self.seed, self.numSamples, n)
+        self.ctx.render(self.numSamples + 1, rf)
+        self.numSamples += n
+
+    def sampleComplete(self):                    # :144-156
+        if not self.isSampleComplete:
+            self.isSampleComplete = self.numSamples >= self.samplePerPixel
+            if self.isSampleComplete:
+                self.ctx.sync()
+                self.lastDispatchTime = self.ctx.last_render_ns() // 1_000_000
+                self.finishTime = int((time.time() - self._start) * 1000)
+                for fn in self._listeners:
+                    fn()
+        return self.isSampleComplete
