@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -61,6 +62,7 @@ struct rt_ctx {
     bool uv_always = false;
     bool validated = false;
     uint64_t last_ns = 0;
+    int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
 };
 
 namespace {
@@ -261,6 +263,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RT_ERR_DEVICE;
     if (n_devices <= 0 || n_devices > count) return RT_ERR_INVALID_ARG;
     rt_ctx* c = new rt_ctx();
+    if (const char* v = std::getenv("RT_KERNEL_VARIANT")) c->variant = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
         Device& d = c->devs[i];
@@ -471,6 +474,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     if (c->host_buf[RT_BIND_LIGHTS].size() >= 4) std::memcpy(&lc, c->host_buf[RT_BIND_LIGHTS].data(), 4);
     a.lights_count = lc;
     a.uv_always = c->uv_always;
+    a.variant = c->variant;
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
     a.max_depth = c->max_depth;

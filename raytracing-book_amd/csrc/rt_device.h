@@ -48,7 +48,7 @@ struct rt_kernel_args {
     const int32_t* lights;
     int n_nodes, lights_count;
     int uv_always;       // a medium samples an image texture: keep sphere uv current (Q9)
-    int pad0;
+    int variant;         // kernel structure variant (A/B; 0 = default)
     rt_dtex tex[8];
     rt_camera_ubo cam;
     float background[3];

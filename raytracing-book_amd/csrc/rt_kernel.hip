@@ -58,9 +58,10 @@ struct UvSrc {
 __device__ __forceinline__ v3 f3(float4 v) { return mk3(v.x, v.y, v.z); }
 
 // ------------------------------------------------------------- primitives
-// hitting.glsl:17-47 (uv deferred)
-__device__ __forceinline__ bool sphere_hit(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
-                                           float tmax, HitRec& rec) {
+// hitting.glsl:17-47 — root only.  Callers that need the surface compute
+// p = o + d*t, then (deferred to the final closest hit) the outward normal.
+__device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
+                                         float tmax, float& t) {
     float4 A = sp[0], B = sp[1];
     v3 center = add3(f3(A), scale3(f3(B), time));
     v3 oc = sub3(o, center);
@@ -74,12 +75,17 @@ __device__ __forceinline__ bool sphere_hit(const float4* __restrict__ sp, float 
         root = (-half_b + sq) / a;
         if (!(tmin < root && root < tmax)) return false;
     }
-    rec.t = root;
-    rec.p = add3(o, scale3(d, root));
+    t = root;
+    return true;
+}
+
+// the rest of hit_sphere (hitting.glsl:39-42) for a hit at rec.p
+__device__ __forceinline__ void sphere_surface(const float4* __restrict__ sp, float time, v3 d, HitRec& rec) {
+    float4 A = sp[0], B = sp[1];
+    v3 center = add3(f3(A), scale3(f3(B), time));
     v3 on = divs3(sub3(rec.p, center), B.w);
     rec.front = g_dot(d, on) < 0.0f;
     rec.normal = rec.front ? on : neg3(on);
-    return true;
 }
 
 // hitting.glsl:90-133
@@ -130,25 +136,27 @@ __device__ __forceinline__ bool box_hit(const float4* __restrict__ b, v3 o, v3 d
     return has;
 }
 
-// hitting.glsl:148-160
-__device__ bool boundary_hit(const KP& P, int idx, int type, v3 o, v3 d, float a, float time, float tmin, float tmax,
-                             HitRec& rec) {
+// hitting.glsl:148-160 (the medium only reads rec.t of its boundary hits)
+__device__ __forceinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3 d, float a, float time, float tmin, float tmax,
+                           float& t) {
     v2 ab;
+    HitRec r;
     if (type == RT_MODEL_SPHERE)
-        return sphere_hit(reinterpret_cast<const float4*>(P.spheres + idx), time, o, d, a, tmin, tmax, rec);
-    if (type == RT_MODEL_QUAD) return quad_hit(reinterpret_cast<const float4*>(P.quads + idx), o, d, tmin, tmax, rec, ab);
-    if (type == RT_MODEL_BOX) return box_hit(reinterpret_cast<const float4*>(P.boxes + idx), o, d, tmin, tmax, rec, ab);
-    return false;
+        return sphere_t(reinterpret_cast<const float4*>(P.spheres + idx), time, o, d, a, tmin, tmax, t);
+    bool h = false;
+    if (type == RT_MODEL_QUAD) h = quad_hit(reinterpret_cast<const float4*>(P.quads + idx), o, d, tmin, tmax, r, ab);
+    else if (type == RT_MODEL_BOX) h = box_hit(reinterpret_cast<const float4*>(P.boxes + idx), o, d, tmin, tmax, r, ab);
+    if (h) t = r.t;
+    return h;
 }
 
 // hitting.glsl:162-193
-__device__ bool medium_hit(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin, float tmax, Rng& g,
+__device__ __forceinline__ bool medium_hit(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin, float tmax, Rng& g,
                            HitRec& rec) {
     const rt_medium m = P.media[idx];
-    HitRec r1, r2;
-    if (!boundary_hit(P, m.boundary_idx, m.boundary_type, o, d, a, time, -RT_INFINITY, RT_INFINITY, r1)) return false;
-    if (!boundary_hit(P, m.boundary_idx, m.boundary_type, o, d, a, time, r1.t + 0.0001f, RT_INFINITY, r2)) return false;
-    float t1 = r1.t, t2 = r2.t;
+    float t1, t2;
+    if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, -RT_INFINITY, RT_INFINITY, t1)) return false;
+    if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, t1 + 0.0001f, RT_INFINITY, t2)) return false;
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
@@ -175,8 +183,49 @@ __device__ __forceinline__ void slab(float mn, float mx, float o, float inv, flo
     hi = (b < hi) ? b : hi;
 }
 
-// compute.glsl:226-266 over the threaded BVH
-__device__ bool trace(const KP& P, v3 o, v3 d, float time, Rng& g, HitRec& rec, int& htype, int& hidx, UvSrc& uvs) {
+// Test the two prims of a leaf (compute.glsl:247-256), left then right.
+__device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a, float time,
+                                           float tmin, float& tmax, Rng& g, HitRec& rec, int& htype, int& hidx,
+                                           UvSrc& uvs, bool& has) {
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        int ty = (int)((meta >> (16 + 4 * s)) & 0xFu);
+        int ix = (int)((prims >> (16 * s)) & 0xFFFFu);
+        if (ty == RT_MODEL_SPHERE) {
+            float t;
+            if (sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t)) {
+                has = true; tmax = t; htype = ty; hidx = ix;
+                rec.t = t;
+                rec.p = add3(o, scale3(d, t));
+                uvs.kind = 1; uvs.idx = ix; uvs.p = rec.p;
+            }
+        } else if (ty == RT_MODEL_QUAD) {
+            v2 ab;
+            if (quad_hit(reinterpret_cast<const float4*>(P.quads + ix), o, d, tmin, tmax, rec, ab)) {
+                has = true; tmax = rec.t; htype = ty; hidx = ix;
+                uvs.kind = 2; uvs.ab = ab;
+            }
+        } else if (ty == RT_MODEL_BOX) {
+            v2 ab;
+            if (box_hit(reinterpret_cast<const float4*>(P.boxes + ix), o, d, tmin, tmax, rec, ab)) {
+                has = true; tmax = rec.t; htype = ty; hidx = ix;
+                uvs.kind = 2; uvs.ab = ab;
+            }
+        } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
+            if (medium_hit(P, ix, o, d, a, time, tmin, tmax, g, rec)) {
+                has = true; tmax = rec.t; htype = ty; hidx = ix;
+            }
+        }
+    }
+}
+
+// compute.glsl:226-266 over the threaded BVH.  The node sequence of every lane
+// is the reference's; only how a wave interleaves its lanes differs:
+//   WHILE_WHILE: lanes advance through inner/missed nodes until each holds a
+//                hit leaf (or is done), then leaves are tested together;
+//   else       : one node per iteration, leaf tests inline (if-if).
+template <bool WHILE_WHILE>
+__device__ __forceinline__ bool trace(const KP& P, v3 o, v3 d, float time, Rng& g, HitRec& rec, int& htype, int& hidx, UvSrc& uvs) {
     if (P.n_nodes == 0) return false;
     float tmin = 0.001f, tmax = RT_INFINITY;
     v3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -184,48 +233,45 @@ __device__ bool trace(const KP& P, v3 o, v3 d, float time, Rng& g, HitRec& rec, 
     bool has = false;
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(P.nodes);
     uint32_t i = 0;
-    while (i != RT_NODE_END) {
-        float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
-        uint32_t meta = __float_as_uint(n1.z);
-        uint32_t prims = __float_as_uint(n1.w);
-        float lo = tmin, hi = tmax;
-        slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-        slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-        slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-        uint32_t skip = meta & 0xFFFFu;
-        if (hi <= lo) { i = skip; continue; }
-        uint32_t ltype = (meta >> 16) & 0xFu;
-        if (ltype == 0) { i = i + 1; continue; }
-        uint32_t types[2] = {ltype, (meta >> 20) & 0xFu};
-        uint32_t idxs[2] = {prims & 0xFFFFu, prims >> 16};
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            int ty = (int)types[s], ix = (int)idxs[s];
-            if (ty == RT_MODEL_SPHERE) {
-                if (sphere_hit(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, rec)) {
-                    has = true; tmax = rec.t; htype = ty; hidx = ix;
-                    uvs.kind = 1; uvs.idx = ix; uvs.p = rec.p;
-                }
-            } else if (ty == RT_MODEL_QUAD) {
-                v2 ab;
-                if (quad_hit(reinterpret_cast<const float4*>(P.quads + ix), o, d, tmin, tmax, rec, ab)) {
-                    has = true; tmax = rec.t; htype = ty; hidx = ix;
-                    uvs.kind = 2; uvs.ab = ab;
-                }
-            } else if (ty == RT_MODEL_BOX) {
-                v2 ab;
-                if (box_hit(reinterpret_cast<const float4*>(P.boxes + ix), o, d, tmin, tmax, rec, ab)) {
-                    has = true; tmax = rec.t; htype = ty; hidx = ix;
-                    uvs.kind = 2; uvs.ab = ab;
-                }
-            } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
-                if (medium_hit(P, ix, o, d, a, time, tmin, tmax, g, rec)) {
-                    has = true; tmax = rec.t; htype = ty; hidx = ix;
-                }
+    if (WHILE_WHILE) {
+        for (;;) {
+            uint32_t meta = 0, prims = 0;
+            bool leaf = false;
+            while (i != RT_NODE_END) {
+                float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
+                meta = __float_as_uint(n1.z);
+                prims = __float_as_uint(n1.w);
+                float lo = tmin, hi = tmax;
+                slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+                slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+                slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+                if (hi <= lo) { i = meta & 0xFFFFu; continue; }
+                if (((meta >> 16) & 0xFu) == 0) { i = i + 1; continue; }
+                leaf = true;
+                break;
             }
+            if (!leaf) break;
+            leaf_prims(P, meta, prims, o, d, a, time, tmin, tmax, g, rec, htype, hidx, uvs, has);
+            i = meta & 0xFFFFu;
         }
-        i = skip;
+    } else {
+        while (i != RT_NODE_END) {
+            float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
+            uint32_t meta = __float_as_uint(n1.z);
+            uint32_t prims = __float_as_uint(n1.w);
+            float lo = tmin, hi = tmax;
+            slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+            slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+            slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+            uint32_t skip = meta & 0xFFFFu;
+            if (hi <= lo) { i = skip; continue; }
+            if (((meta >> 16) & 0xFu) == 0) { i = i + 1; continue; }
+            leaf_prims(P, meta, prims, o, d, a, time, tmin, tmax, g, rec, htype, hidx, uvs, has);
+            i = skip;
+        }
     }
+    if (has && htype == RT_MODEL_SPHERE)
+        sphere_surface(reinterpret_cast<const float4*>(P.spheres + hidx), time, d, rec);
     return has;
 }
 
@@ -250,7 +296,7 @@ __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
 }
 
 // texture.glsl:38-77 (Perlin table: 6 x 256 R32F, row-major width 6)
-__device__ float perlin_noise(const rt_dtex& T, v3 p) {
+__device__ __forceinline__ float perlin_noise(const rt_dtex& T, v3 p) {
     float u = p.x - floorf(p.x);
     float v = p.y - floorf(p.y);
     float w = p.z - floorf(p.z);
@@ -295,7 +341,7 @@ __device__ __forceinline__ v2 sphere_uv(v3 p) {
     return r;
 }
 
-__device__ v2 resolve_uv(const KP& P, const UvSrc& s, float time) {
+__device__ __forceinline__ v2 resolve_uv(const KP& P, const UvSrc& s, float time) {
     if (s.kind == 2) return s.ab;
     if (s.kind == 1) {
         const float4* sp = reinterpret_cast<const float4*>(P.spheres + s.idx);
@@ -308,7 +354,7 @@ __device__ v2 resolve_uv(const KP& P, const UvSrc& s, float time) {
 }
 
 // texture.glsl:112-132
-__device__ v3 texture_color(const KP& P, v3 p, int id, const UvSrc& uvs, float time) {
+__device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvSrc& uvs, float time) {
     int detail_i = id & 0xFFF;
     int index = (id >> 12) & 0xFFFF;
     int type = (id >> 28) & 0xF;
@@ -387,10 +433,10 @@ __device__ __forceinline__ v3 rand_unit_vec(Rng& g) {
 }
 
 // pdf.glsl:11-24
-__device__ float sphere_light_pdf(const KP& P, int idx, v3 o, v3 d, float time) {
+__device__ __forceinline__ float sphere_light_pdf(const KP& P, int idx, v3 o, v3 d, float time) {
     const float4* sp = reinterpret_cast<const float4*>(P.spheres + idx);
-    HitRec r;
-    if (!sphere_hit(sp, time, o, d, g_dot(d, d), 0.001f, RT_INFINITY, r)) return 0.0f;
+    float t;
+    if (!sphere_t(sp, time, o, d, g_dot(d, d), 0.001f, RT_INFINITY, t)) return 0.0f;
     float4 A = sp[0], B = sp[1];
     v3 pc = sub3(f3(A), o);
     float d2 = g_dot(pc, pc);
@@ -400,7 +446,7 @@ __device__ float sphere_light_pdf(const KP& P, int idx, v3 o, v3 d, float time) 
 }
 
 // pdf.glsl:41-51
-__device__ float quad_light_pdf(const KP& P, int idx, v3 o, v3 d) {
+__device__ __forceinline__ float quad_light_pdf(const KP& P, int idx, v3 o, v3 d) {
     const float4* q = reinterpret_cast<const float4*>(P.quads + idx);
     HitRec r;
     v2 ab;
@@ -411,7 +457,7 @@ __device__ float quad_light_pdf(const KP& P, int idx, v3 o, v3 d) {
 }
 
 // pdf.glsl:58-81
-__device__ float lights_pdf_value(const KP& P, v3 o, v3 d, float time) {
+__device__ __forceinline__ float lights_pdf_value(const KP& P, v3 o, v3 d, float time) {
     float weight = 1.0f / (float)P.lights_count;
     float sum = 0.0f;
     for (int i = 0; i < P.lights_count; i++) {
@@ -426,7 +472,7 @@ __device__ float lights_pdf_value(const KP& P, v3 o, v3 d, float time) {
 }
 
 // pdf.glsl:83-96 (+ random.glsl:71-80, pdf.glsl:26-30, :53-56); no light -> vec3(0) (Q1)
-__device__ v3 lights_random(const KP& P, v3 o, Rng& g) {
+__device__ __forceinline__ v3 lights_random(const KP& P, v3 o, Rng& g) {
     float r = 0.0f + rnd(g) * ((float)(P.lights_count - 1 + 1) - 0.0f);
     int li = rt_f2i(floorf(r));
     if (li < 0 || li >= P.lights_count) return mk3s(0.0f);
@@ -460,116 +506,173 @@ __device__ v3 lights_random(const KP& P, v3 o, Rng& g) {
 }
 
 // ------------------------------------------------------------- ray_color
-// compute.glsl:298-343
-__device__ v3 ray_color(const KP& P, v3 o, v3 d, float time, Rng& g) {
-    v3 acc = mk3s(1.0f);
-    v3 final_color = mk3s(0.0f);
+// Per-lane path state carried between bounces (ray_color's locals).
+struct Path {
+    v3 o, d, acc;
+    float time;
+    Rng g;
     HitRec rec;
-    rec.t = 0.0f; rec.p = mk3s(0.0f); rec.normal = mk3s(0.0f); rec.front = false;
     UvSrc uvs;
-    uvs.kind = 0; uvs.idx = 0; uvs.p = mk3s(0.0f); uvs.ab.x = 0.0f; uvs.ab.y = 0.0f;
-    for (int depth = 0; depth < P.max_depth; depth++) {
-        int htype = 0, hidx = 0;
-        bool dir_zero = (d.x == 0.0f) & (d.y == 0.0f) & (d.z == 0.0f);
-        // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
-        if (dir_zero || !trace(P, o, d, time, g, rec, htype, hidx, uvs)) {
-            final_color = mul3(acc, mk3(P.background[0], P.background[1], P.background[2]));
-            break;
-        }
-        // set_material_properties for the closest hit (compute.glsl:197-224)
-        int material, tex_id;
-        v3 emis = mk3s(0.0f);
-        if (htype == RT_MODEL_SPHERE) {
-            const float4* sp = reinterpret_cast<const float4*>(P.spheres + hidx);
-            float4 A = sp[0], C = sp[2];
-            material = __float_as_int(C.w); tex_id = __float_as_int(A.w);
-            if (rec.front) emis = f3(C);
-        } else if (htype == RT_MODEL_CONSTANT_MEDIUM) {
-            material = P.media[hidx].phase_material; tex_id = P.media[hidx].texture_id;
-        } else {
-            const float4* q = (htype == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + hidx)
-                                                      : reinterpret_cast<const float4*>(P.boxes + hidx);
-            material = __float_as_int(q[1].w); tex_id = __float_as_int(q[2].w);
-            if (rec.front) emis = f3(q[4]);
-        }
-        // scatter (scatter.glsl:43-98)
-        int mid = (material >> 16) & 0xFFFF;
-        bool skip_pdf = false, should = false;
-        if (mid == RT_MAT_DIFFUSE_LIGHT) {
-            final_color = mul3(acc, emis);
-            break;
-        }
-        if (mid == RT_MAT_LAMBERTIAN) {
-            float r1 = rnd(g);
-            float r2 = rnd(g);
-            float phi = 2.0f * RT_PI * r1;
-            float s, c;
-            g_sincos(phi, &s, &c);
-            v3 cd = mk3(c * sqrtf(r2), s * sqrtf(r2), sqrtf(1.0f - r2));
-            d = transform_onb(cd, rec.normal);
-            should = true;
-        } else if (mid == RT_MAT_METAL) {
-            float fuzz = (float)(material & 0xFFFF) / 65535.0f;
-            d = g_reflect(d, rec.normal);
-            v3 n = g_normalize(d);
-            d = add3(n, scale3(rand_unit_vec(g), fuzz));
-            should = g_dot(d, rec.normal) > 0.0f;
-            skip_pdf = true;
-        } else if (mid == RT_MAT_DIELECTRIC) {
-            float nior = (float)(material & 0xFFFF) / 65535.0f;
-            float eta = g_mix(1.0f, 2.5f, nior);
-            if (rec.front) eta = 1.0f / eta;
-            d = g_normalize(d);
-            float cos_t = g_min(g_dot(neg3(d), rec.normal), 1.0f);
-            float sin_t = sqrtf(1.0f - cos_t * cos_t);
-            bool cannot = eta * sin_t > 1.0f;
-            bool refl = cannot;
-            if (!refl) {
-                float r0 = (1.0f - eta) / (1.0f + eta);
-                r0 = r0 * r0;
-                float rf = r0 + (1.0f - r0) * g_pow5(1.0f - cos_t);
-                refl = rf > rnd(g);
-            }
-            d = refl ? g_reflect(d, rec.normal) : g_refract(d, rec.normal, eta);
-            should = true;
-            skip_pdf = true;
-        } else if (mid == RT_MAT_ISOTROPIC) {
-            d = rand_unit_vec(g);
-            should = true;
-        }
-        if ((fabsf(d.x) < 1e-8f) & (fabsf(d.y) < 1e-8f) & (fabsf(d.z) < 1e-8f)) d = rec.normal;
-        if (!should) {
-            final_color = mul3(acc, emis);
-            break;
-        }
-        o = rec.p;
-        if (skip_pdf) {
-            acc = mul3(acc, texture_color(P, rec.p, tex_id, uvs, time));
-            continue;
-        }
-        if (rnd(g) < 0.5f) d = lights_random(P, o, g);
-        float lpdf = (P.lights_count > 0) ? lights_pdf_value(P, o, d, time) : 0.0f;
-        float mpdf;
-        if (mid == RT_MAT_LAMBERTIAN) mpdf = g_max(0.0f, g_normalize1(g_dot(d, rec.normal)) / RT_PI);
-        else if (mid == RT_MAT_ISOTROPIC) mpdf = 1.0f / (4.0f * RT_PI);
-        else mpdf = 0.0f;
-        float pdf = 0.5f * lpdf + 0.5f * mpdf;
-        if (pdf == 0.0f) {
-            final_color = mul3(acc, emis);
-            break;
-        }
-        float spdf;
-        if (mid == RT_MAT_LAMBERTIAN) spdf = g_max(0.0f, g_dot(rec.normal, g_normalize(d)) / RT_PI);
-        else if (mid == RT_MAT_ISOTROPIC) spdf = 1.0f / (4.0f * RT_PI);
-        else spdf = 0.0f;
-        v3 att = texture_color(P, rec.p, tex_id, uvs, time);
-        acc = mul3(acc, divs3(scale3(att, spdf), pdf));
+    int depth;
+};
+
+// One iteration of ray_color's loop (compute.glsl:304-340).  Returns true when
+// the path ended, with its color in `result`.
+template <bool WW>
+__device__ __forceinline__ bool bounce(const KP& P, Path& S, v3& result) {
+    if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
+        result = mk3s(0.0f);
+        return true;
     }
-    return final_color;
+    S.depth++;
+    int htype = 0, hidx = 0;
+    v3 d = S.d;
+    bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
+    // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
+    if (dir_zero || !trace<WW>(P, S.o, d, S.time, S.g, S.rec, htype, hidx, S.uvs)) {
+        result = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
+        return true;
+    }
+    const HitRec& rec = S.rec;
+    // set_material_properties for the closest hit (compute.glsl:197-224)
+    int material, tex_id;
+    v3 emis = mk3s(0.0f);
+    if (htype == RT_MODEL_SPHERE) {
+        const float4* sp = reinterpret_cast<const float4*>(P.spheres + hidx);
+        float4 A = sp[0], C = sp[2];
+        material = __float_as_int(C.w);
+        tex_id = __float_as_int(A.w);
+        if (rec.front) emis = f3(C);
+    } else if (htype == RT_MODEL_CONSTANT_MEDIUM) {
+        material = P.media[hidx].phase_material;
+        tex_id = P.media[hidx].texture_id;
+    } else {
+        const float4* q = (htype == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + hidx)
+                                                  : reinterpret_cast<const float4*>(P.boxes + hidx);
+        material = __float_as_int(q[1].w);
+        tex_id = __float_as_int(q[2].w);
+        if (rec.front) emis = f3(q[4]);
+    }
+    // scatter (scatter.glsl:43-98)
+    int mid = (material >> 16) & 0xFFFF;
+    bool skip_pdf = false, should = false;
+    if (mid == RT_MAT_DIFFUSE_LIGHT) {
+        result = mul3(S.acc, emis);
+        return true;
+    }
+    Rng& g = S.g;
+    if (mid == RT_MAT_LAMBERTIAN) {
+        float r1 = rnd(g);
+        float r2 = rnd(g);
+        float phi = 2.0f * RT_PI * r1;
+        float s, c;
+        g_sincos(phi, &s, &c);
+        v3 cd = mk3(c * sqrtf(r2), s * sqrtf(r2), sqrtf(1.0f - r2));
+        d = transform_onb(cd, rec.normal);
+        should = true;
+    } else if (mid == RT_MAT_METAL) {
+        float fuzz = (float)(material & 0xFFFF) / 65535.0f;
+        d = g_reflect(d, rec.normal);
+        v3 n = g_normalize(d);
+        d = add3(n, scale3(rand_unit_vec(g), fuzz));
+        should = g_dot(d, rec.normal) > 0.0f;
+        skip_pdf = true;
+    } else if (mid == RT_MAT_DIELECTRIC) {
+        float nior = (float)(material & 0xFFFF) / 65535.0f;
+        float eta = g_mix(1.0f, 2.5f, nior);
+        if (rec.front) eta = 1.0f / eta;
+        d = g_normalize(d);
+        float cos_t = g_min(g_dot(neg3(d), rec.normal), 1.0f);
+        float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        bool refl = eta * sin_t > 1.0f;
+        if (!refl) {
+            float r0 = (1.0f - eta) / (1.0f + eta);
+            r0 = r0 * r0;
+            float rf = r0 + (1.0f - r0) * g_pow5(1.0f - cos_t);
+            refl = rf > rnd(g);
+        }
+        d = refl ? g_reflect(d, rec.normal) : g_refract(d, rec.normal, eta);
+        should = true;
+        skip_pdf = true;
+    } else if (mid == RT_MAT_ISOTROPIC) {
+        d = rand_unit_vec(g);
+        should = true;
+    }
+    if ((fabsf(d.x) < 1e-8f) && (fabsf(d.y) < 1e-8f) && (fabsf(d.z) < 1e-8f)) d = rec.normal;
+    if (!should) {
+        result = mul3(S.acc, emis);
+        return true;
+    }
+    S.o = rec.p;
+    if (skip_pdf) {
+        S.acc = mul3(S.acc, texture_color(P, rec.p, tex_id, S.uvs, S.time));
+        S.d = d;
+        return false;
+    }
+    if (rnd(g) < 0.5f) d = lights_random(P, S.o, g);
+    float lpdf = (P.lights_count > 0) ? lights_pdf_value(P, S.o, d, S.time) : 0.0f;
+    float mpdf;
+    if (mid == RT_MAT_LAMBERTIAN) mpdf = g_max(0.0f, g_normalize1(g_dot(d, rec.normal)) / RT_PI);
+    else if (mid == RT_MAT_ISOTROPIC) mpdf = 1.0f / (4.0f * RT_PI);
+    else mpdf = 0.0f;
+    float pdf = 0.5f * lpdf + 0.5f * mpdf;
+    if (pdf == 0.0f) {
+        result = mul3(S.acc, emis);
+        return true;
+    }
+    float spdf;
+    if (mid == RT_MAT_LAMBERTIAN) spdf = g_max(0.0f, g_dot(rec.normal, g_normalize(d)) / RT_PI);
+    else if (mid == RT_MAT_ISOTROPIC) spdf = 1.0f / (4.0f * RT_PI);
+    else spdf = 0.0f;
+    v3 att = texture_color(P, rec.p, tex_id, S.uvs, S.time);
+    S.acc = mul3(S.acc, divs3(scale3(att, spdf), pdf));
+    S.d = d;
+    return false;
 }
 
-// compute.glsl:345-358, all frames of the launch per work-item
-__global__ void __launch_bounds__(256) render_kernel(const KP* __restrict__ Pp) {
+// Camera ray of frame `frame_count` (compute.glsl:345-350, random.glsl:19-30,82-100).
+__device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count, float rf, float fx, float fy, v3 base) {
+    const rt_camera_ubo& C = P.cam;
+    v3 du = ld3(C.pixel_delta_u), dv = ld3(C.pixel_delta_v), cpos = ld3(C.camera_pos);
+    Rng& g = S.g;
+    g.rf = rf;
+    g.px = fx;
+    g.py = fy;
+    S.time = rnd(g);
+    float col = g_mod((float)frame_count, P.sqrt_spp);
+    float layer = (float)frame_count / P.sqrt_spp;
+    float base_x = (col + 0.5f) * P.recip_sqrt_spp;
+    float base_y = (layer + 0.5f) * P.recip_sqrt_spp;
+    float jx = (rnd(g) - 0.5f) * P.recip_sqrt_spp;
+    float jy = (rnd(g) - 0.5f) * P.recip_sqrt_spp;
+    float spx = base_x + jx - 0.5f;
+    float spy = base_y + jy - 0.5f;
+    v3 coord = add3(base, add3(scale3(du, spx), scale3(dv, spy)));
+    v3 o = cpos;
+    if (!(C.defocus_angle <= 0.0f)) {
+        float dx, dy;
+        for (;;) {
+            dx = -1.0f + rnd(g) * 2.0f;
+            dy = -1.0f + rnd(g) * 2.0f;
+            v3 p = mk3(dx, dy, 0.0f);
+            if (g_dot(p, p) < 1.0f) break;
+        }
+        o = add3(add3(cpos, scale3(ld3(C.defocus_disk_u), dx)), scale3(ld3(C.defocus_disk_v), dy));
+    }
+    S.o = o;
+    S.d = sub3(coord, o);
+    S.acc = mk3s(1.0f);
+    S.depth = 0;
+    S.rec.t = 0.0f; S.rec.p = mk3s(0.0f); S.rec.normal = mk3s(0.0f); S.rec.front = false;
+    S.uvs.kind = 0; S.uvs.idx = 0; S.uvs.p = mk3s(0.0f); S.uvs.ab.x = 0.0f; S.uvs.ab.y = 0.0f;
+}
+
+// compute.glsl:345-358 for all frames of the launch.  Path regeneration: a lane
+// whose path ended starts its next frame at once, so a wave never idles until
+// its longest path of a frame is done; each pixel still runs its frames in order
+// and applies the running mean per frame.
+template <bool WW, int MINW>
+__global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     int x = blockIdx.x * 16 + threadIdx.x;
     int lr = blockIdx.y * 16 + threadIdx.y;
@@ -579,46 +682,29 @@ __global__ void __launch_bounds__(256) render_kernel(const KP* __restrict__ Pp) 
     float4* px = reinterpret_cast<float4*>(P.image) + (size_t)lr * P.width + x;
     float4 prev = *px;
     const rt_camera_ubo& C = P.cam;
-    v3 ul = ld3(C.up_left), du = ld3(C.pixel_delta_u), dv = ld3(C.pixel_delta_v);
     float fx = (float)x, fy = (float)y;
-    // get_norm_coord without the jitter term (same for every frame)
-    v3 base = add3(add3(ul, scale3(du, fx)), scale3(dv, fy));
-    v3 cpos = ld3(C.camera_pos);
-    for (int f = 0; f < P.n_frames; f++) {
-        int frame_count = P.first_frame + f;
-        Rng g;
-        g.rf = P.rand_factors[f];
-        g.px = fx;
-        g.py = fy;
-        float time = rnd(g);
-        // pixel_sample_square (random.glsl:82-100)
-        float col = g_mod((float)frame_count, P.sqrt_spp);
-        float layer = (float)frame_count / P.sqrt_spp;
-        float base_x = (col + 0.5f) * P.recip_sqrt_spp;
-        float base_y = (layer + 0.5f) * P.recip_sqrt_spp;
-        float jx = (rnd(g) - 0.5f) * P.recip_sqrt_spp;
-        float jy = (rnd(g) - 0.5f) * P.recip_sqrt_spp;
-        float spx = base_x + jx - 0.5f;
-        float spy = base_y + jy - 0.5f;
-        v3 coord = add3(base, add3(scale3(du, spx), scale3(dv, spy)));
-        v3 o = cpos;
-        if (!(C.defocus_angle <= 0.0f)) {   // defocus_disk_sample (random.glsl:19-30)
-            float dx, dy;
-            for (;;) {
-                dx = -1.0f + rnd(g) * 2.0f;
-                dy = -1.0f + rnd(g) * 2.0f;
-                v3 p = mk3(dx, dy, 0.0f);
-                if (g_dot(p, p) < 1.0f) break;
-            }
-            o = add3(add3(cpos, scale3(ld3(C.defocus_disk_u), dx)), scale3(ld3(C.defocus_disk_v), dy));
+    // get_norm_coord (compute.glsl:268-283) before its jitter term: per pixel
+    v3 base = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
+    Path S;
+    int f = 0;
+    bool fresh = true;
+    for (;;) {
+        if (fresh) {
+            if (f >= P.n_frames) break;
+            start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, base);
+            fresh = false;
         }
-        v3 d = sub3(coord, o);
-        v3 cur = ray_color(P, o, d, time, g);
-        float n1 = (float)(frame_count - 1), n = (float)frame_count;
-        prev.x = (prev.x * n1 + cur.x) / n;
-        prev.y = (prev.y * n1 + cur.y) / n;
-        prev.z = (prev.z * n1 + cur.z) / n;
-        prev.w = 1.0f;
+        v3 cur;
+        if (bounce<WW>(P, S, cur)) {
+            int fc = P.first_frame + f;
+            float n1 = (float)(fc - 1), n = (float)fc;
+            prev.x = (prev.x * n1 + cur.x) / n;
+            prev.y = (prev.y * n1 + cur.y) / n;
+            prev.z = (prev.z * n1 + cur.z) / n;
+            prev.w = 1.0f;
+            f++;
+            fresh = true;
+        }
     }
     *px = prev;
 }
@@ -651,7 +737,17 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess) return -1;
     dim3 block(16, 16);
     dim3 grid((a.width + 15) / 16, (a.local_rows + 15) / 16);
-    hipLaunchKernelGGL(render_kernel, grid, block, 0, (hipStream_t)stream, (const rt_kernel_args*)dargs);
+    // variant (A/B only): 0 while-while default occupancy, 1 if-if, 2/3 while-while
+    // with >= 4 / >= 5 waves per SIMD, 4 if-if with >= 4 waves per SIMD.
+    const rt_kernel_args* d = (const rt_kernel_args*)dargs;
+    hipStream_t st = (hipStream_t)stream;
+    switch (a.variant) {
+        case 1: hipLaunchKernelGGL((render_kernel<false, 1>), grid, block, 0, st, d); break;
+        case 2: hipLaunchKernelGGL((render_kernel<true, 4>), grid, block, 0, st, d); break;
+        case 3: hipLaunchKernelGGL((render_kernel<true, 5>), grid, block, 0, st, d); break;
+        case 4: hipLaunchKernelGGL((render_kernel<false, 4>), grid, block, 0, st, d); break;
+        default: hipLaunchKernelGGL((render_kernel<true, 1>), grid, block, 0, st, d); break;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

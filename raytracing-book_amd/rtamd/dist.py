@@ -37,7 +37,7 @@ def gather_image(local_block, height, world, stripe_rows):
     """All-gather the [padded_rows, W, 4] blocks and de-interleave (rank 0 and others)."""
     if world == 1:
         rows = local_rows(height, 0, 1, stripe_rows)
-        return local_block[:rows]
+        return local_block[:rows].cpu().numpy()
     padded = padded_local_rows(height, world, stripe_rows)
     assert local_block.shape[0] == padded
     if dist.get_backend() == "nccl":

@@ -1,0 +1,65 @@
+"""Interleaved in-process A/B of kernel structure variants (RT_KERNEL_VARIANT).
+
+Every variant must produce the same bits; timings are HIP-event device time of
+one rt_render call (1 launch) per round, reported as median/min over rounds.
+usage: python tools/ab_variants.py [--variants 0,1,2] [--rounds 5] [--scene 8]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracing-book_amd"))
+import numpy as np  # noqa: E402
+import rtamd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1,2,3,4")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--scene", type=int, default=8)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--frames", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=5)
+    a = ap.parse_args()
+    variants = [int(v) for v in a.variants.split(",")]
+    scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
+    ctxs = {}
+    for v in variants:
+        os.environ["RT_KERNEL_VARIANT"] = str(v)
+        c = rtamd.RenderContext(devices=(0,))
+        c.upload_scene(scene)
+        c.set_params(max_depth=a.depth, spp=4096)
+        c.resize(a.width, a.height)
+        ctxs[v] = c
+    rf = rtamd.frame_rand_factors(1, 0, a.frames)
+    times = {v: [] for v in variants}
+    ref = None
+    for r in range(a.rounds + 1):
+        for v in variants:
+            c = ctxs[v]
+            c.resize(a.width, a.height)      # zero the image: same inputs every round
+            c.render(1, rf)
+            c.sync()
+            ns = c.last_render_ns()
+            if r == 0:   # warm-up round; check bits
+                img = c.read_image()
+                if ref is None:
+                    ref = img
+                else:
+                    same = np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(
+                        img.view(np.uint32)[~np.isnan(img)], ref.view(np.uint32)[~np.isnan(ref)])
+                    print(f"variant {v}: bits {'identical' if same else 'DIFFER'} to variant {variants[0]}")
+                continue
+            times[v].append(ns / 1e6)
+    samples = a.width * a.height * a.frames
+    for v in variants:
+        med = statistics.median(times[v])
+        print(f"variant {v}: median {med:.2f} ms  min {min(times[v]):.2f} ms  -> {samples / med / 1e3:.1f} Msamples/s")
+
+
+if __name__ == "__main__":
+    main()

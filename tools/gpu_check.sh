@@ -21,6 +21,9 @@ for s in $STEPS; do
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    ab)    run ab 600 python tools/ab_variants.py ${AB_ARGS:-} ;;
+    list)  run pmc_list 120 rocprofv3 -L ;;
+    pmc)   run pmc 900 python tools/pmc_profile.py ${PMC_ARGS:-} ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
   esac
 done

@@ -1,0 +1,83 @@
+"""Collect rocprofv3 PMC counters for the render kernel, one counter group per
+pass (separate rocprofv3 runs, --kernel-trace only alongside --pmc), and write a
+summary JSON.  Run on the GPU box:  python tools/pmc_profile.py --out profiles/pmc_r01.json
+HBM traffic per the MI355X guide: FETCH_SIZE under-reports coalesced reads by 2x
+on gfx950 and is in KB; we report FETCH_SIZE*1024 (raw) and the x2-corrected
+bound, plus WRITE_SIZE*1024."""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+GROUPS = [
+    ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SMEM", "SQ_INSTS_LDS"],
+    ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"],
+    ["SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU_TRANS_F32"],
+    ["FETCH_SIZE"],
+    ["WRITE_SIZE"],
+    ["TCC_HIT_sum", "TCC_MISS_sum"],
+    ["TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum"],
+    ["GRBM_GUI_ACTIVE", "GRBM_COUNT"],
+]
+
+
+def available():
+    try:
+        out = subprocess.run(["rocprofv3", "-L"], capture_output=True, text=True, timeout=120).stdout
+    except Exception:
+        return None
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "pmc.json"))
+    ap.add_argument("--target", default="--scene 8 --frames 64")
+    a = ap.parse_args()
+    listing = available() or ""
+    res = {}
+    os.makedirs(os.path.join(REPO, "gpurun_out", "pmc"), exist_ok=True)
+    for gi, grp in enumerate(GROUPS):
+        grp = [c for c in grp if not listing or c in listing]
+        if not grp:
+            continue
+        d = os.path.join(REPO, "gpurun_out", "pmc", f"g{gi}")
+        cmd = ["timeout", "-k", "10", "300", "rocprofv3", "--kernel-trace", "--pmc", *grp, "--output-format", "csv",
+               "-d", d, "-o", "run", "--", sys.executable, os.path.join(REPO, "tools", "render_once.py"),
+               *a.target.split()]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        print("group", gi, grp, "rc", r.returncode, flush=True)
+        if r.returncode not in (0,):
+            print(r.stderr[-2000:], flush=True)
+            if r.returncode in (124, 134, 137, 139):
+                break
+            continue
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if "render_kernel" not in row.get("Kernel_Name", ""):
+                        continue
+                    name = row.get("Counter_Name")
+                    val = float(row.get("Counter_Value", 0))
+                    res.setdefault(name, 0.0)
+                    res[name] += val
+    if "FETCH_SIZE" in res:
+        res["hbm_read_bytes_raw"] = res["FETCH_SIZE"] * 1024
+        res["hbm_read_bytes_x2"] = res["FETCH_SIZE"] * 1024 * 2
+    if "WRITE_SIZE" in res:
+        res["hbm_write_bytes"] = res["WRITE_SIZE"] * 1024
+    if "SQ_THREAD_CYCLES_VALU" in res and "SQ_ACTIVE_INST_VALU" in res and res["SQ_ACTIVE_INST_VALU"]:
+        res["valu_lane_utilization"] = res["SQ_THREAD_CYCLES_VALU"] / (64.0 * res["SQ_ACTIVE_INST_VALU"])
+    res["target"] = a.target
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
