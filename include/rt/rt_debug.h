@@ -19,6 +19,13 @@ int rt_debug_eval_builtin(int device, int fn, const float* x, const float* y, fl
  * (32-byte rt_dnode records); out may be NULL to query the count. */
 int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t out_cap, int* n_out);
 
+/* Diagnostic build of the render kernel with wave-level region timers and
+ * active-lane counters (never used for timed numbers).  enable=1 switches the
+ * context to it and zeroes the counters; read returns n <= 64 counters. */
+struct rt_ctx;
+int rt_debug_enable_stats(struct rt_ctx* ctx, int enable);
+int rt_debug_read_stats(struct rt_ctx* ctx, unsigned long long* out, int n);
+
 /* Number of visible HIP devices (0 when none). */
 int rt_debug_device_count(void);
 

@@ -36,6 +36,12 @@ struct Device {
     DevBuf nodes, spheres, quads, boxes, media, lights, tex[8];
     DevBuf image;            // internal image
     DevBuf args;             // rt_kernel_args slot in device memory
+    DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
+    DevBuf counter;          // persistent-kernel tile counter
+    static constexpr int kRing = 8;
+    rt_kernel_args* ring = nullptr;   // pinned host staging slots for async arg uploads
+    hipEvent_t ring_ev[kRing] = {};
+    int ring_pos = 0;
     float* image_ptr = nullptr;  // active image (internal or bound)
     bool image_bound = false;
     int rank = 0, world = 1;     // stripe assignment of this device
@@ -79,8 +85,25 @@ int set_err(rt_ctx* c, int code, const std::string& m) {
             return set_err(ctx, RT_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_));   \
     } while (0)
 
+// Every host<->device transfer and fill is ordered on the device's render stream
+// (which may be non-blocking or caller-owned) and completed before returning, so
+// it can neither overlap a queued render nor race the next one.
+int h2d(rt_ctx* c, Device& d, void* dst, const void* src, size_t n) {
+    if (!n) return RT_OK;
+    HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(c, hipStreamSynchronize(d.stream));
+    return RT_OK;
+}
+int d2h(rt_ctx* c, Device& d, void* dst, const void* src, size_t n) {
+    if (!n) return RT_OK;
+    HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(c, hipStreamSynchronize(d.stream));
+    return RT_OK;
+}
+
 int dev_alloc_copy(rt_ctx* c, Device& d, DevBuf& b, const void* src, size_t n) {
     HIPCHK(c, hipSetDevice(d.id));
+    HIPCHK(c, hipStreamSynchronize(d.stream));
     if (b.ptr && b.bytes < n) {
         HIPCHK(c, hipFree(b.ptr));
         b.ptr = nullptr;
@@ -90,8 +113,7 @@ int dev_alloc_copy(rt_ctx* c, Device& d, DevBuf& b, const void* src, size_t n) {
         HIPCHK(c, hipMalloc(&b.ptr, n));
         b.bytes = n;
     }
-    if (n > 0) HIPCHK(c, hipMemcpy(b.ptr, src, n, hipMemcpyHostToDevice));
-    return RT_OK;
+    return h2d(c, d, b.ptr, src, n);
 }
 
 void dev_free(DevBuf& b) {
@@ -236,6 +258,7 @@ int validate(rt_ctx* c) {
 
 int alloc_image(rt_ctx* c, Device& d) {
     HIPCHK(c, hipSetDevice(d.id));
+    HIPCHK(c, hipStreamSynchronize(d.stream));
     d.local_rows = local_rows_of(c->height, d.rank, d.world, c->stripe_rows);
     d.padded_rows = padded_rows_of(c->height, d.world, c->stripe_rows);
     size_t bytes = (size_t)d.padded_rows * c->width * 16;
@@ -243,7 +266,8 @@ int alloc_image(rt_ctx* c, Device& d) {
     if (bytes) {
         HIPCHK(c, hipMalloc(&d.image.ptr, bytes));
         d.image.bytes = bytes;
-        HIPCHK(c, hipMemset(d.image.ptr, 0, bytes));
+        HIPCHK(c, hipMemsetAsync(d.image.ptr, 0, bytes, d.stream));
+        HIPCHK(c, hipStreamSynchronize(d.stream));
     }
     d.image_ptr = (float*)d.image.ptr;
     d.image_bound = false;
@@ -287,7 +311,10 @@ int rt_destroy(rt_ctx* c) {
         (void)hipSetDevice(d.id);
         (void)hipStreamSynchronize(d.stream);
         dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
-        dev_free(d.lights); dev_free(d.image); dev_free(d.args);
+        dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter);
+        if (d.ring) (void)hipHostFree(d.ring);
+        for (auto& e : d.ring_ev)
+            if (e) (void)hipEventDestroy(e);
         for (auto& t : d.tex) dev_free(t);
         if (d.ev_start) (void)hipEventDestroy(d.ev_start);
         if (d.ev_stop) (void)hipEventDestroy(d.ev_stop);
@@ -499,21 +526,32 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             a.tex[t].is_float = c->tex_format[t] == RT_TEX_R32F;
         }
         a.image = d.image_ptr;
+        a.stats = (unsigned long long*)d.stats.ptr;
         a.local_rows = d.local_rows;
         a.rank = d.rank;
         a.world = d.world;
         if (!d.args.ptr) {
+            HIPCHK(c, hipMalloc(&d.counter.ptr, 256));
+            d.counter.bytes = 256;
             HIPCHK(c, hipMalloc(&d.args.ptr, sizeof(rt_kernel_args)));
             d.args.bytes = sizeof(rt_kernel_args);
+            HIPCHK(c, hipHostMalloc((void**)&d.ring, sizeof(rt_kernel_args) * Device::kRing, hipHostMallocDefault));
+            for (auto& e : d.ring_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
+        a.tile_counter = (int*)d.counter.ptr;
         HIPCHK(c, hipEventRecord(d.ev_start, d.stream));
         for (int f0 = 0; f0 < n_frames; f0 += RT_MAX_FRAMES_PER_LAUNCH) {
             int nf = std::min(RT_MAX_FRAMES_PER_LAUNCH, n_frames - f0);
             a.first_frame = first_frame + f0;
             a.n_frames = nf;
             std::memcpy(a.rand_factors, rand_factors + f0, sizeof(float) * nf);
-            if (rt_launch_render(a, (rt_kernel_args*)d.args.ptr, d.stream))
-                return set_err(c, RT_ERR_DEVICE, "kernel launch failed");
+            int slot = d.ring_pos++ % Device::kRing;
+            HIPCHK(c, hipEventSynchronize(d.ring_ev[slot]));   // the copy that last used this slot is done
+            d.ring[slot] = a;
+            if (rt_launch_render(d.ring[slot], (rt_kernel_args*)d.args.ptr, d.stream))
+                return set_err(c, RT_ERR_DEVICE, std::string("kernel launch failed: ") +
+                                                     hipGetErrorString(hipGetLastError()));
+            HIPCHK(c, hipEventRecord(d.ring_ev[slot], d.stream));
         }
         HIPCHK(c, hipEventRecord(d.ev_stop, d.stream));
         d.timed = true;
@@ -555,8 +593,7 @@ int rt_read_image(rt_ctx* c, float* rgba) {
     if (c->devs.size() == 1) {
         Device& d = c->devs[0];
         HIPCHK(c, hipSetDevice(d.id));
-        HIPCHK(c, hipMemcpy(rgba, d.image_ptr, (size_t)d.local_rows * c->width * 16, hipMemcpyDeviceToHost));
-        return RT_OK;
+        return d2h(c, d, rgba, d.image_ptr, (size_t)d.local_rows * c->width * 16);
     }
     // multi-device context: gather stripes to the host and de-interleave
     int ndev = (int)c->devs.size();
@@ -565,8 +602,9 @@ int rt_read_image(rt_ctx* c, float* rgba) {
     for (int k = 0; k < ndev; k++) {
         Device& d = c->devs[k];
         HIPCHK(c, hipSetDevice(d.id));
-        HIPCHK(c, hipMemcpy(g.data() + (size_t)k * padded * c->width * 4, d.image_ptr,
-                            (size_t)d.local_rows * c->width * 16, hipMemcpyDeviceToHost));
+        int r2 = d2h(c, d, g.data() + (size_t)k * padded * c->width * 4, d.image_ptr,
+                     (size_t)d.local_rows * c->width * 16);
+        if (r2) return r2;
     }
     return rt_deinterleave_rows(g.data(), c->width, c->height, ndev, c->stripe_rows, rgba);
 }
@@ -581,7 +619,8 @@ int rt_write_image(rt_ctx* c, const float* rgba) {
         std::vector<float> local((size_t)d.local_rows * c->width * 4);
         // pick this device's rows from the (process-local) image
         if (c->devs.size() == 1) {
-            HIPCHK(c, hipMemcpy(d.image_ptr, rgba, local.size() * 4, hipMemcpyHostToDevice));
+            int r2 = h2d(c, d, d.image_ptr, rgba, local.size() * 4);
+            if (r2) return r2;
             continue;
         }
         int n_stripes = (c->height + c->stripe_rows - 1) / c->stripe_rows;
@@ -589,7 +628,8 @@ int rt_write_image(rt_ctx* c, const float* rgba) {
         for (int s = d.rank; s < n_stripes; s += d.world)
             for (int y = s * c->stripe_rows; y < std::min(c->height, (s + 1) * c->stripe_rows); y++, lr++)
                 std::memcpy(&local[lr * c->width * 4], rgba + (size_t)y * c->width * 4, (size_t)c->width * 16);
-        HIPCHK(c, hipMemcpy(d.image_ptr, local.data(), local.size() * 4, hipMemcpyHostToDevice));
+        int r2 = h2d(c, d, d.image_ptr, local.data(), local.size() * 4);
+        if (r2) return r2;
     }
     return RT_OK;
 }
@@ -646,6 +686,36 @@ int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t ou
     if (out) {
         if (out_cap < dn.size() * sizeof(rt_dnode)) return RT_ERR_INVALID_ARG;
         std::memcpy(out, dn.data(), dn.size() * sizeof(rt_dnode));
+    }
+    return RT_OK;
+}
+
+int rt_debug_enable_stats(rt_ctx* c, int on) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    for (Device& d : c->devs) {
+        HIPCHK(c, hipSetDevice(d.id));
+        HIPCHK(c, hipStreamSynchronize(d.stream));
+        if (on && !d.stats.ptr) {
+            HIPCHK(c, hipMalloc(&d.stats.ptr, 64 * sizeof(unsigned long long)));
+            d.stats.bytes = 64 * sizeof(unsigned long long);
+        }
+        if (d.stats.ptr) HIPCHK(c, hipMemsetAsync(d.stats.ptr, 0, d.stats.bytes, d.stream));
+        HIPCHK(c, hipStreamSynchronize(d.stream));
+    }
+    c->variant = on ? ((c->variant == 0 || c->variant >= 10) ? 19 : 9) : 0;
+    return RT_OK;
+}
+
+int rt_debug_read_stats(rt_ctx* c, unsigned long long* out, int n) {
+    if (!c || !out || n <= 0 || n > 64) return RT_ERR_INVALID_ARG;
+    std::memset(out, 0, sizeof(unsigned long long) * n);
+    for (Device& d : c->devs) {
+        if (!d.stats.ptr) continue;
+        HIPCHK(c, hipSetDevice(d.id));
+        std::vector<unsigned long long> tmp(n);
+        int r = d2h(c, d, tmp.data(), d.stats.ptr, sizeof(unsigned long long) * n);
+        if (r) return r;
+        for (int i = 0; i < n; i++) out[i] += tmp[i];
     }
     return RT_OK;
 }

@@ -18,6 +18,7 @@
 
 #define RT_MAX_FRAMES_PER_LAUNCH 256
 #define RT_NODE_END 0xFFFFu
+#define RT_LDS_NODE_BYTES (64 * 1024)   // stage the BVH in LDS when it fits (2 workgroups/CU)
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
 // continues at index+1 (its RIGHT child, which the reference visits first
@@ -60,6 +61,8 @@ struct rt_kernel_args {
     int local_rows;
     int rank, world, stripe_rows;
     int first_frame, n_frames;
+    unsigned long long* stats;   // diagnostic counters (stats variant only)
+    int* tile_counter;           // persistent variants: next 8x8 tile (zeroed per launch)
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
 };
 

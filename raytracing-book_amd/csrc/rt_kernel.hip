@@ -3,20 +3,23 @@
 // Semantics: the reference's per-invocation compute shader
 // (S/raytrace/compute.glsl:345-358 + S/utils/*.glsl), bit-exact with the CPU
 // oracle given the shared GLSL built-in definitions (include/rt/rt_glsl.h) and
-// -ffp-contract=off.  Structure (MI355X-first, every change value-preserving):
-//   * one work-item per pixel, 16x16 workgroups (4 waves of 16x4 pixels), and
-//     ALL frames of a launch looped in-register: the RGBA32F running mean
-//     (compute.glsl:355) is applied per frame exactly, but the image is read
-//     and written once per launch instead of once per frame;
-//   * stackless traversal of a threaded BVH (rt_dnode) that visits the
-//     reference's node sequence (stack pops, right child first) without the
-//     int stack[64] the GLSL keeps in scratch;
-//   * per-ray constants hoisted: 1/dir per axis and dot(dir,dir) (identical
-//     values, computed once instead of per node / per sphere);
-//   * deferred shading: set_material_properties (compute.glsl:197-224) is
-//     resolved once for the final closest hit, and texture_color (pure, no
-//     rand()) only when the bounce actually uses the attenuation;
-//   * sphere uv (acos/atan2) only when an image texture will read it.
+// -ffp-contract=off.  Structure (MI355X-first; every change value-preserving):
+//   * persistent grid: each workgroup stages the threaded BVH in LDS once and
+//     each wave pulls 8x8 pixel tiles from a device-wide counter;
+//   * a work-item owns one pixel and loops over ALL frames of the launch with
+//     path regeneration (a finished path starts the pixel's next frame at
+//     once); the RGBA32F running mean (compute.glsl:355) is applied per frame
+//     exactly, but the image is read/written once per launch;
+//   * stackless walk of a threaded BVH (rt_dnode) visiting the reference's node
+//     sequence (stack pops, right child first) without the int stack[64];
+//   * lean hit record during the walk (t, type, index, box face, uv source);
+//     p, normal and front face are rebuilt once for the closest hit with the
+//     reference's own expressions, and set_material_properties
+//     (compute.glsl:197-224) / texture_color run once per bounce, only when
+//     the value is used;
+//   * per-ray constants hoisted (1/dir, dot(dir,dir)); a box's six face planes
+//     are divided independently before the sequential acceptance; a medium's
+//     two boundary hits share one quadratic.
 // rand() consumption order is identical to the reference.
 #include <hip/hip_runtime.h>
 
@@ -27,39 +30,66 @@ namespace {
 
 typedef rt_kernel_args KP;
 
-struct Rng {
-    float rf, px, py;
-};
+__device__ __forceinline__ v3 f3(float4 v) { return mk3(v.x, v.y, v.z); }
 
-// random.glsl:2-7
-__device__ __forceinline__ float rnd(Rng& g) {
-    g.rf += 0.001f;
+// ---- diagnostic statistics (stats variants only; never in a timed build) ----
+// Wave-level: the first active lane adds into the wave's LDS counters, so a
+// region is charged once per wave execution whatever its EXEC mask.
+enum {
+    ST_TOTAL = 0, ST_START_CYC, ST_START_IT, ST_START_LN, ST_NODE_CYC, ST_NODE_IT, ST_NODE_LN, ST_LEAF_CYC,
+    ST_LEAF_IT, ST_LEAF_LN, ST_SPH_LN, ST_QUAD_LN, ST_BOX_LN, ST_MED_LN, ST_SHADE_CYC, ST_SHADE_IT, ST_SHADE_LN,
+    ST_SPH_IT, ST_QUAD_IT, ST_BOX_IT, ST_MED_IT, ST_N
+};
+__device__ __forceinline__ bool first_active_lane() {
+    unsigned long long m = __ballot(1);
+    return (unsigned)__lane_id() == (unsigned)(__ffsll((long long)m) - 1);
+}
+__device__ __forceinline__ void st_add(unsigned long long* st, int slot, unsigned long long v) {
+    if (first_active_lane()) atomicAdd(&st[slot], v);
+}
+__device__ __forceinline__ void st_lanes(unsigned long long* st, int it_slot, int ln_slot) {
+    unsigned long long m = __ballot(1);
+    if (first_active_lane()) {
+        atomicAdd(&st[it_slot], 1ull);
+        atomicAdd(&st[ln_slot], (unsigned long long)__popcll(m));
+    }
+}
+__device__ __forceinline__ void st_pred(unsigned long long* st, bool pred, int it_slot, int ln_slot) {
+    unsigned long long m = __ballot(pred);
+    if (m && first_active_lane()) {
+        atomicAdd(&st[it_slot], 1ull);
+        atomicAdd(&st[ln_slot], (unsigned long long)__popcll(m));
+    }
+}
+
+// ------------------------------------------------------------------ rand()
+// random.glsl:2-7; `rf` is the invocation's running rand_factor.
+__device__ __forceinline__ float rnd(float& rf, float px, float py) {
+    rf += 0.001f;
     v2 co;
-    co.x = g.px + g.rf;
-    co.y = g.py + g.rf;
+    co.x = px + rf;
+    co.y = py + rf;
     v2 k = {12.9898f, 78.233f};
     return g_fract(g_sin(g_dot2(co, k)) * 43758.5453123f);
 }
 
-struct HitRec {
-    float t;
-    v3 p, normal;
-    bool front;
-};
-
-// Source of hit_record.uv (compute.glsl:62): last successful sphere or quad hit.
+// Source of hit_record.uv (compute.glsl:62): the last successful sphere or quad
+// hit of the sample (it persists across bounces; media do not write it).
 struct UvSrc {
-    int kind;   // 0 none, 1 sphere (idx, p), 2 quad (a, b)
-    int idx;
-    v3 p;
-    v2 ab;
+    int kind_idx;   // kind in bits 16.. (0 none, 1 sphere, 2 quad), sphere index in bits 0..15
+    float a, b, c;  // sphere: hit point p; quad: (alpha, beta)
 };
 
-__device__ __forceinline__ v3 f3(float4 v) { return mk3(v.x, v.y, v.z); }
+// Closest hit of one walk.
+struct Hit {
+    float t;
+    int type, idx, face;
+    int uv_kind_idx;    // uv written during this walk (kind 0 = none)
+    float uv_a, uv_b;   // sphere: t of that hit; quad: (alpha, beta)
+};
 
 // ------------------------------------------------------------- primitives
-// hitting.glsl:17-47 — root only.  Callers that need the surface compute
-// p = o + d*t, then (deferred to the final closest hit) the outward normal.
+// hitting.glsl:17-38 — the root only.
 __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
                                          float tmax, float& t) {
     float4 A = sp[0], B = sp[1];
@@ -79,29 +109,14 @@ __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float ti
     return true;
 }
 
-// the rest of hit_sphere (hitting.glsl:39-42) for a hit at rec.p
-__device__ __forceinline__ void sphere_surface(const float4* __restrict__ sp, float time, v3 d, HitRec& rec) {
-    float4 A = sp[0], B = sp[1];
-    v3 center = add3(f3(A), scale3(f3(B), time));
-    v3 on = divs3(sub3(rec.p, center), B.w);
-    rec.front = g_dot(d, on) < 0.0f;
-    rec.normal = rec.front ? on : neg3(on);
-}
-
-// hitting.glsl:90-133
-__device__ __forceinline__ bool quad_hit(const float4* __restrict__ q, v3 o, v3 d, float tmin, float tmax,
-                                         HitRec& rec, v2& ab) {
-    float4 Q0 = q[0];
-    v3 n = f3(Q0);
-    float denom = g_dot(n, d);
-    if (fabsf(denom) < 1e-8f) return false;
-    float t = (Q0.w - g_dot(n, o)) / denom;
-    if (!(tmin <= t && t <= tmax)) return false;
+// hitting.glsl:103-124: is the plane hit at t inside the quad? (alpha, beta) out.
+__device__ __forceinline__ bool quad_interior(const float4* __restrict__ q, v3 o, v3 d, float t, float& alpha,
+                                              float& beta) {
     float4 Q1 = q[1], Q2 = q[2], Q3 = q[3];
     v3 inter = add3(o, scale3(d, t));
     v3 ph = sub3(inter, f3(Q1));
     v3 u = f3(Q2), v = f3(Q3);
-    float delta, alpha, beta;
+    float delta;
     if ((delta = u.x * v.y - u.y * v.x) != 0.0f) {
         alpha = (ph.x * v.y - ph.y * v.x) / delta;
         beta = (ph.y * u.x - ph.x * u.y) / delta;
@@ -113,66 +128,116 @@ __device__ __forceinline__ bool quad_hit(const float4* __restrict__ q, v3 o, v3 
         alpha = (ph.y * v.z - ph.z * v.y) / delta;
         beta = (ph.z * u.y - ph.y * u.z) / delta;
     }
-    if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return false;
-    ab.x = alpha;
-    ab.y = beta;
-    rec.t = t;
-    rec.p = inter;
-    rec.front = g_dot(d, n) < 0.0f;
-    rec.normal = rec.front ? n : neg3(n);
+    return (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+}
+
+// hitting.glsl:90-133 without the record writes.
+__device__ __forceinline__ bool quad_test(const float4* __restrict__ q, v3 o, v3 d, float tmin, float tmax, float& t,
+                                          float& alpha, float& beta) {
+    float4 Q0 = q[0];
+    v3 n = f3(Q0);
+    float denom = g_dot(n, d);
+    if (fabsf(denom) < 1e-8f) return false;
+    float tt = (Q0.w - g_dot(n, o)) / denom;
+    if (!(tmin <= tt && tt <= tmax)) return false;
+    if (!quad_interior(q, o, d, tt, alpha, beta)) return false;
+    t = tt;
     return true;
 }
 
-// hitting.glsl:135-146
-__device__ __forceinline__ bool box_hit(const float4* __restrict__ b, v3 o, v3 d, float tmin, float tmax, HitRec& rec,
-                                        v2& ab) {
-    bool has = false;
+// hitting.glsl:135-146.  The six faces' plane parameters t_i do not depend on
+// the shrinking ray_t.max, so they are divided independently (ILP); faces are
+// then accepted in the reference order with the reference's sequential test
+// tmin <= t_i <= current max, and only those reach the interior test — the same
+// tests on the same values, so the same result.
+__device__ __forceinline__ bool box_test(const float4* __restrict__ b, v3 o, v3 d, float tmin, float tmax, float& t,
+                                         int& face, float& alpha, float& beta) {
+    float ti[6];
+    unsigned cand = 0;
+#pragma unroll
     for (int i = 0; i < 6; i++) {
-        if (quad_hit(b + 5 * i, o, d, tmin, tmax, rec, ab)) {
-            tmax = rec.t;
-            has = true;
+        float4 pl = b[5 * i];
+        v3 n = f3(pl);
+        float denom = g_dot(n, d);
+        ti[i] = (pl.w - g_dot(n, o)) / denom;   // unused when |denom| < 1e-8
+        if (!(fabsf(denom) < 1e-8f) && (tmin <= ti[i] && ti[i] <= tmax)) cand |= 1u << i;
+    }
+    bool has = false;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        if ((cand >> i) & 1u) {
+            float al, be;
+            if (ti[i] <= tmax && quad_interior(b + 5 * i, o, d, ti[i], al, be)) {
+                tmax = ti[i];
+                t = ti[i];
+                face = i;
+                alpha = al;
+                beta = be;
+                has = true;
+            }
         }
     }
     return has;
 }
 
-// hitting.glsl:148-160 (the medium only reads rec.t of its boundary hits)
-__device__ __forceinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3 d, float a, float time, float tmin, float tmax,
-                           float& t) {
-    v2 ab;
-    HitRec r;
+// hitting.glsl:148-160 for a medium boundary (only rec.t is read, :165-178).
+// Out of line: only quad/box boundaries (scene 7) come here.
+__device__ __noinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3 d, float a, float time, float tmin,
+                                           float tmax, float& t) {
+    float al, be;
+    int face;
     if (type == RT_MODEL_SPHERE)
         return sphere_t(reinterpret_cast<const float4*>(P.spheres + idx), time, o, d, a, tmin, tmax, t);
-    bool h = false;
-    if (type == RT_MODEL_QUAD) h = quad_hit(reinterpret_cast<const float4*>(P.quads + idx), o, d, tmin, tmax, r, ab);
-    else if (type == RT_MODEL_BOX) h = box_hit(reinterpret_cast<const float4*>(P.boxes + idx), o, d, tmin, tmax, r, ab);
-    if (h) t = r.t;
-    return h;
+    if (type == RT_MODEL_QUAD) return quad_test(reinterpret_cast<const float4*>(P.quads + idx), o, d, tmin, tmax, t, al, be);
+    if (type == RT_MODEL_BOX)
+        return box_test(reinterpret_cast<const float4*>(P.boxes + idx), o, d, tmin, tmax, t, face, al, be);
+    return false;
 }
 
-// hitting.glsl:162-193
-__device__ __forceinline__ bool medium_hit(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin, float tmax, Rng& g,
-                           HitRec& rec) {
+// hitting.glsl:162-193 — returns the hit distance t.
+__device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin,
+                                            float tmax, float& rf, float px, float py, float& t) {
     const rt_medium m = P.media[idx];
     float t1, t2;
-    if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, -RT_INFINITY, RT_INFINITY, t1)) return false;
-    if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, t1 + 0.0001f, RT_INFINITY, t2)) return false;
+    if (m.boundary_type == RT_MODEL_SPHERE) {
+        // Both boundary hit_sphere calls (:165, :168) see the same ray and sphere:
+        // the quadratic and both roots are computed once, then each call's root
+        // selection is applied to its own interval.
+        const float4* sp = reinterpret_cast<const float4*>(P.spheres + m.boundary_idx);
+        float4 A = sp[0], B = sp[1];
+        v3 center = add3(f3(A), scale3(f3(B), time));
+        v3 oc = sub3(o, center);
+        float half_b = g_dot(oc, d);
+        float c = g_dot(oc, oc) - B.w * B.w;
+        float disc = half_b * half_b - a * c;
+        if (disc < 0.0f) return false;
+        float sq = sqrtf(disc);
+        float r_lo = (-half_b - sq) / a;
+        float r_hi = (-half_b + sq) / a;
+        if (-RT_INFINITY < r_lo && r_lo < RT_INFINITY) t1 = r_lo;
+        else if (-RT_INFINITY < r_hi && r_hi < RT_INFINITY) t1 = r_hi;
+        else return false;
+        float lo2 = t1 + 0.0001f;
+        if (lo2 < r_lo && r_lo < RT_INFINITY) t2 = r_lo;
+        else if (lo2 < r_hi && r_hi < RT_INFINITY) t2 = r_hi;
+        else return false;
+    } else {
+        if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, -RT_INFINITY, RT_INFINITY, t1)) return false;
+        if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, t1 + 0.0001f, RT_INFINITY, t2)) return false;
+    }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
     if (t1 < 0.0f) t1 = 0.0f;
     float len = sqrtf(a);   // length(ray.dir); a == dot(dir, dir)
     float inside = (t2 - t1) * len;
-    float hd = m.neg_inv_density * g_log(rnd(g));
+    float hd = m.neg_inv_density * g_log(rnd(rf, px, py));
     if (hd > inside) return false;
-    rec.t = t1 + hd / len;
-    rec.p = add3(o, scale3(d, rec.t));
-    rec.normal = mk3(1.0f, 0.0f, 0.0f);
-    rec.front = true;
+    t = t1 + hd / len;
     return true;
 }
 
-// hitting.glsl:55-76 for one axis (branch-free; same assignments)
+// hitting.glsl:55-76 for one axis (branch-free; the same assignments)
 __device__ __forceinline__ void slab(float mn, float mx, float o, float inv, float& lo, float& hi) {
     float t0 = (mn - o) * inv;
     float t1 = (mx - o) * inv;
@@ -183,61 +248,65 @@ __device__ __forceinline__ void slab(float mn, float mx, float o, float inv, flo
     hi = (b < hi) ? b : hi;
 }
 
-// Test the two prims of a leaf (compute.glsl:247-256), left then right.
+// The two prims of a leaf (compute.glsl:247-256), left then right.
+template <bool STATS>
 __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a, float time,
-                                           float tmin, float& tmax, Rng& g, HitRec& rec, int& htype, int& hidx,
-                                           UvSrc& uvs, bool& has) {
-#pragma unroll
+                                           float tmin, float& tmax, float& rf, float px, float py, Hit& h, bool& has,
+                                           unsigned long long* st) {
+#pragma unroll 1
     for (int s = 0; s < 2; s++) {
         int ty = (int)((meta >> (16 + 4 * s)) & 0xFu);
         int ix = (int)((prims >> (16 * s)) & 0xFFFFu);
+        if (STATS) {
+            st_pred(st, ty == RT_MODEL_SPHERE, ST_SPH_IT, ST_SPH_LN);
+            st_pred(st, ty == RT_MODEL_QUAD, ST_QUAD_IT, ST_QUAD_LN);
+            st_pred(st, ty == RT_MODEL_BOX, ST_BOX_IT, ST_BOX_LN);
+            st_pred(st, ty == RT_MODEL_CONSTANT_MEDIUM, ST_MED_IT, ST_MED_LN);
+        }
+        float t = 0.0f, al = 0.0f, be = 0.0f;
+        int face = 0;
+        bool hit = false;
         if (ty == RT_MODEL_SPHERE) {
-            float t;
-            if (sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t)) {
-                has = true; tmax = t; htype = ty; hidx = ix;
-                rec.t = t;
-                rec.p = add3(o, scale3(d, t));
-                uvs.kind = 1; uvs.idx = ix; uvs.p = rec.p;
-            }
+            hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t);
+            if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
         } else if (ty == RT_MODEL_QUAD) {
-            v2 ab;
-            if (quad_hit(reinterpret_cast<const float4*>(P.quads + ix), o, d, tmin, tmax, rec, ab)) {
-                has = true; tmax = rec.t; htype = ty; hidx = ix;
-                uvs.kind = 2; uvs.ab = ab;
-            }
+            hit = quad_test(reinterpret_cast<const float4*>(P.quads + ix), o, d, tmin, tmax, t, al, be);
+            if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_BOX) {
-            v2 ab;
-            if (box_hit(reinterpret_cast<const float4*>(P.boxes + ix), o, d, tmin, tmax, rec, ab)) {
-                has = true; tmax = rec.t; htype = ty; hidx = ix;
-                uvs.kind = 2; uvs.ab = ab;
-            }
+            hit = box_test(reinterpret_cast<const float4*>(P.boxes + ix), o, d, tmin, tmax, t, face, al, be);
+            if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
-            if (medium_hit(P, ix, o, d, a, time, tmin, tmax, g, rec)) {
-                has = true; tmax = rec.t; htype = ty; hidx = ix;
-            }
+            hit = medium_test(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
+        }
+        if (hit) {
+            has = true;
+            tmax = t;
+            h.t = t; h.type = ty; h.idx = ix; h.face = face;
         }
     }
 }
 
-// compute.glsl:226-266 over the threaded BVH.  The node sequence of every lane
-// is the reference's; only how a wave interleaves its lanes differs:
+// compute.glsl:226-266 over the threaded BVH.  Each lane's node sequence is the
+// reference's; only the interleaving of a wave's lanes differs:
 //   WHILE_WHILE: lanes advance through inner/missed nodes until each holds a
-//                hit leaf (or is done), then leaves are tested together;
+//                hit leaf (or is done), then the leaves are tested together;
 //   else       : one node per iteration, leaf tests inline (if-if).
-template <bool WHILE_WHILE>
-__device__ __forceinline__ bool trace(const KP& P, v3 o, v3 d, float time, Rng& g, HitRec& rec, int& htype, int& hidx, UvSrc& uvs) {
+template <bool WHILE_WHILE, bool STATS>
+__device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ nodes, v3 o, v3 d, float time,
+                                      float& rf, float px, float py, Hit& h, unsigned long long* st) {
     if (P.n_nodes == 0) return false;
     float tmin = 0.001f, tmax = RT_INFINITY;
     v3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float a = g_dot(d, d);
     bool has = false;
-    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(P.nodes);
     uint32_t i = 0;
     if (WHILE_WHILE) {
         for (;;) {
             uint32_t meta = 0, prims = 0;
             bool leaf = false;
+            unsigned long long t0 = STATS ? clock64() : 0;
             while (i != RT_NODE_END) {
+                if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
                 float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
                 meta = __float_as_uint(n1.z);
                 prims = __float_as_uint(n1.w);
@@ -250,8 +319,12 @@ __device__ __forceinline__ bool trace(const KP& P, v3 o, v3 d, float time, Rng& 
                 leaf = true;
                 break;
             }
+            if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
             if (!leaf) break;
-            leaf_prims(P, meta, prims, o, d, a, time, tmin, tmax, g, rec, htype, hidx, uvs, has);
+            unsigned long long t1 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+            leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
             i = meta & 0xFFFFu;
         }
     } else {
@@ -266,12 +339,10 @@ __device__ __forceinline__ bool trace(const KP& P, v3 o, v3 d, float time, Rng& 
             uint32_t skip = meta & 0xFFFFu;
             if (hi <= lo) { i = skip; continue; }
             if (((meta >> 16) & 0xFu) == 0) { i = i + 1; continue; }
-            leaf_prims(P, meta, prims, o, d, a, time, tmin, tmax, g, rec, htype, hidx, uvs, has);
+            leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
             i = skip;
         }
     }
-    if (has && htype == RT_MODEL_SPHERE)
-        sphere_surface(reinterpret_cast<const float4*>(P.spheres + hidx), time, d, rec);
     return has;
 }
 
@@ -295,7 +366,7 @@ __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
     return t[0];
 }
 
-// texture.glsl:38-77 (Perlin table: 6 x 256 R32F, row-major width 6)
+// texture.glsl:38-77 with perlin_interp (19-36) fused; Hermite applied twice (Q6)
 __device__ __forceinline__ float perlin_noise(const rt_dtex& T, v3 p) {
     float u = p.x - floorf(p.x);
     float v = p.y - floorf(p.y);
@@ -306,7 +377,6 @@ __device__ __forceinline__ float perlin_noise(const rt_dtex& T, v3 p) {
     int i = rt_f2i(floorf(p.x));
     int j = rt_f2i(floorf(p.y));
     int k = rt_f2i(floorf(p.z));
-    // perlin_interp (texture.glsl:19-36), double Hermite as in the reference (Q6)
     float uu = u * u * (3.0f - 2.0f * u);
     float vv = v * v * (3.0f - 2.0f * v);
     float ww = w * w * (3.0f - 2.0f * w);
@@ -342,12 +412,13 @@ __device__ __forceinline__ v2 sphere_uv(v3 p) {
 }
 
 __device__ __forceinline__ v2 resolve_uv(const KP& P, const UvSrc& s, float time) {
-    if (s.kind == 2) return s.ab;
-    if (s.kind == 1) {
-        const float4* sp = reinterpret_cast<const float4*>(P.spheres + s.idx);
+    int kind = s.kind_idx >> 16;
+    if (kind == 2) { v2 r = {s.a, s.b}; return r; }
+    if (kind == 1) {
+        const float4* sp = reinterpret_cast<const float4*>(P.spheres + (s.kind_idx & 0xFFFF));
         float4 A = sp[0], B = sp[1];
         v3 center = add3(f3(A), scale3(f3(B), time));
-        return sphere_uv(sub3(s.p, center));
+        return sphere_uv(sub3(mk3(s.a, s.b, s.c), center));
     }
     v2 z = {0.0f, 0.0f};
     return z;
@@ -377,6 +448,7 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         float scale = ((float)detail_i / 4095.0f) * 100.0f;
         float accum = 0.0f, weight = 1.0f;
         v3 q = p;
+#pragma unroll 1
         for (int o = 0; o < 7; o++) {
             accum += weight * perlin_noise(T, q);
             weight *= 0.5f;
@@ -395,7 +467,8 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         int x0 = rt_f2i(fx), y0 = rt_f2i(fy);
         int x1 = x0 >= T.w - 1 ? T.w - 1 : x0 + 1;
         int y1 = y0 >= T.h - 1 ? T.h - 1 : y0 + 1;
-        x1 = x1 < 0 ? 0 : x1; y1 = y1 < 0 ? 0 : y1;
+        x1 = x1 < 0 ? 0 : x1;
+        y1 = y1 < 0 ? 0 : y1;
         x0 = x0 < 0 ? 0 : (x0 > T.w - 1 ? T.w - 1 : x0);
         y0 = y0 < 0 ? 0 : (y0 > T.h - 1 ? T.h - 1 : y0);
         float t00[3], t10[3], t01[3], t11[3];
@@ -420,12 +493,12 @@ __device__ __forceinline__ v3 transform_onb(v3 vec, v3 normal) {
 }
 
 // random.glsl:40-49
-__device__ __forceinline__ v3 rand_unit_vec(Rng& g) {
+__device__ __forceinline__ v3 rand_unit_vec(float& rf, float px, float py) {
     v3 p;
     for (;;) {
-        float x = -1.0f + rnd(g) * 2.0f;
-        float y = -1.0f + rnd(g) * 2.0f;
-        float z = -1.0f + rnd(g) * 2.0f;
+        float x = -1.0f + rnd(rf, px, py) * 2.0f;
+        float y = -1.0f + rnd(rf, px, py) * 2.0f;
+        float z = -1.0f + rnd(rf, px, py) * 2.0f;
         p = mk3(x, y, z);
         if (g_dot(p, p) < 1.0f) break;
     }
@@ -448,11 +521,13 @@ __device__ __forceinline__ float sphere_light_pdf(const KP& P, int idx, v3 o, v3
 // pdf.glsl:41-51
 __device__ __forceinline__ float quad_light_pdf(const KP& P, int idx, v3 o, v3 d) {
     const float4* q = reinterpret_cast<const float4*>(P.quads + idx);
-    HitRec r;
-    v2 ab;
-    if (!quad_hit(q, o, d, 0.001f, RT_INFINITY, r, ab)) return 0.0f;
-    float d2 = r.t * r.t * g_dot(d, d);
-    float cosine = fabsf(g_dot(d, r.normal) / g_length(d));
+    float t, al, be;
+    if (!quad_test(q, o, d, 0.001f, RT_INFINITY, t, al, be)) return 0.0f;
+    v3 n = f3(q[0]);
+    bool front = g_dot(d, n) < 0.0f;
+    v3 normal = front ? n : neg3(n);
+    float d2 = t * t * g_dot(d, d);
+    float cosine = fabsf(g_dot(d, normal) / g_length(d));
     return d2 / (cosine * q[3].w);
 }
 
@@ -472,8 +547,8 @@ __device__ __forceinline__ float lights_pdf_value(const KP& P, v3 o, v3 d, float
 }
 
 // pdf.glsl:83-96 (+ random.glsl:71-80, pdf.glsl:26-30, :53-56); no light -> vec3(0) (Q1)
-__device__ __forceinline__ v3 lights_random(const KP& P, v3 o, Rng& g) {
-    float r = 0.0f + rnd(g) * ((float)(P.lights_count - 1 + 1) - 0.0f);
+__device__ __forceinline__ v3 lights_random(const KP& P, v3 o, float& rf, float px, float py) {
+    float r = 0.0f + rnd(rf, px, py) * ((float)(P.lights_count - 1 + 1) - 0.0f);
     int li = rt_f2i(floorf(r));
     if (li < 0 || li >= P.lights_count) return mk3s(0.0f);
     int packed = P.lights[li];
@@ -483,8 +558,8 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, Rng& g) {
         float4 A = sp[0], B = sp[1];
         v3 dir = sub3(f3(A), o);
         float d2 = g_dot(dir, dir);
-        float r1 = rnd(g);
-        float r2 = rnd(g);
+        float r1 = rnd(rf, px, py);
+        float r2 = rnd(rf, px, py);
         float z = 1.0f + r2 * (sqrtf(1.0f - B.w * B.w / d2) - 1.0f);
         float phi = 2.0f * RT_PI * r1;
         float s, c;
@@ -496,9 +571,9 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, Rng& g) {
     if (type == RT_MODEL_QUAD) {
         const float4* q = reinterpret_cast<const float4*>(P.quads + idx);
         float4 Q1 = q[1], Q2 = q[2], Q3 = q[3];
-        float r1 = rnd(g);
+        float r1 = rnd(rf, px, py);
         v3 p = add3(f3(Q1), scale3(f3(Q2), r1));
-        float r2 = rnd(g);
+        float r2 = rnd(rf, px, py);
         p = add3(p, scale3(f3(Q3), r2));
         return sub3(p, o);
     }
@@ -509,49 +584,45 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, Rng& g) {
 // Per-lane path state carried between bounces (ray_color's locals).
 struct Path {
     v3 o, d, acc;
-    float time;
-    Rng g;
-    HitRec rec;
+    float time, rf;
     UvSrc uvs;
     int depth;
 };
 
-// One iteration of ray_color's loop (compute.glsl:304-340).  Returns true when
-// the path ended, with its color in `result`.
-template <bool WW>
-__device__ __forceinline__ bool bounce(const KP& P, Path& S, v3& result) {
-    if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
-        result = mk3s(0.0f);
-        return true;
-    }
-    S.depth++;
-    int htype = 0, hidx = 0;
+// The shading half of ray_color's loop body (compute.glsl:310-339) for a hit.
+// Returns true when the path ended, with its color in `result`.
+__device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float px, float py, v3& result) {
     v3 d = S.d;
-    bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
-    // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
-    if (dir_zero || !trace<WW>(P, S.o, d, S.time, S.g, S.rec, htype, hidx, S.uvs)) {
-        result = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
-        return true;
-    }
-    const HitRec& rec = S.rec;
-    // set_material_properties for the closest hit (compute.glsl:197-224)
+    // hit_record of the closest hit: p = ray.o + ray.dir*t (hitting.glsl:39,104,188)
+    v3 p = add3(S.o, scale3(d, h.t));
+    v3 normal;
+    bool front;
     int material, tex_id;
     v3 emis = mk3s(0.0f);
-    if (htype == RT_MODEL_SPHERE) {
-        const float4* sp = reinterpret_cast<const float4*>(P.spheres + hidx);
-        float4 A = sp[0], C = sp[2];
+    if (h.type == RT_MODEL_SPHERE) {   // hitting.glsl:40-42 + compute.glsl:199-204
+        const float4* sp = reinterpret_cast<const float4*>(P.spheres + h.idx);
+        float4 A = sp[0], B = sp[1], C = sp[2];
+        v3 center = add3(f3(A), scale3(f3(B), S.time));
+        v3 on = divs3(sub3(p, center), B.w);
+        front = g_dot(d, on) < 0.0f;
+        normal = front ? on : neg3(on);
         material = __float_as_int(C.w);
         tex_id = __float_as_int(A.w);
-        if (rec.front) emis = f3(C);
-    } else if (htype == RT_MODEL_CONSTANT_MEDIUM) {
-        material = P.media[hidx].phase_material;
-        tex_id = P.media[hidx].texture_id;
-    } else {
-        const float4* q = (htype == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + hidx)
-                                                  : reinterpret_cast<const float4*>(P.boxes + hidx);
-        material = __float_as_int(q[1].w);
-        tex_id = __float_as_int(q[2].w);
-        if (rec.front) emis = f3(q[4]);
+        if (front) emis = f3(C);
+    } else if (h.type == RT_MODEL_CONSTANT_MEDIUM) {   // hitting.glsl:189-190 + compute.glsl:211-216
+        normal = mk3(1.0f, 0.0f, 0.0f);
+        front = true;
+        material = P.media[h.idx].phase_material;
+        tex_id = P.media[h.idx].texture_id;
+    } else {   // quad, or box face h.face (material from quads[0], compute.glsl:217-221)
+        const float4* q0 = (h.type == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + h.idx)
+                                                    : reinterpret_cast<const float4*>(P.boxes + h.idx);
+        v3 n = f3(q0[5 * h.face]);
+        front = g_dot(d, n) < 0.0f;
+        normal = front ? n : neg3(n);
+        material = __float_as_int(q0[1].w);
+        tex_id = __float_as_int(q0[2].w);
+        if (front) emis = f3(q0[4]);
     }
     // scatter (scatter.glsl:43-98)
     int mid = (material >> 16) & 0xFFFF;
@@ -560,59 +631,59 @@ __device__ __forceinline__ bool bounce(const KP& P, Path& S, v3& result) {
         result = mul3(S.acc, emis);
         return true;
     }
-    Rng& g = S.g;
+    float& rf = S.rf;
     if (mid == RT_MAT_LAMBERTIAN) {
-        float r1 = rnd(g);
-        float r2 = rnd(g);
+        float r1 = rnd(rf, px, py);
+        float r2 = rnd(rf, px, py);
         float phi = 2.0f * RT_PI * r1;
         float s, c;
         g_sincos(phi, &s, &c);
         v3 cd = mk3(c * sqrtf(r2), s * sqrtf(r2), sqrtf(1.0f - r2));
-        d = transform_onb(cd, rec.normal);
+        d = transform_onb(cd, normal);
         should = true;
     } else if (mid == RT_MAT_METAL) {
         float fuzz = (float)(material & 0xFFFF) / 65535.0f;
-        d = g_reflect(d, rec.normal);
+        d = g_reflect(d, normal);
         v3 n = g_normalize(d);
-        d = add3(n, scale3(rand_unit_vec(g), fuzz));
-        should = g_dot(d, rec.normal) > 0.0f;
+        d = add3(n, scale3(rand_unit_vec(rf, px, py), fuzz));
+        should = g_dot(d, normal) > 0.0f;
         skip_pdf = true;
     } else if (mid == RT_MAT_DIELECTRIC) {
         float nior = (float)(material & 0xFFFF) / 65535.0f;
         float eta = g_mix(1.0f, 2.5f, nior);
-        if (rec.front) eta = 1.0f / eta;
+        if (front) eta = 1.0f / eta;
         d = g_normalize(d);
-        float cos_t = g_min(g_dot(neg3(d), rec.normal), 1.0f);
+        float cos_t = g_min(g_dot(neg3(d), normal), 1.0f);
         float sin_t = sqrtf(1.0f - cos_t * cos_t);
         bool refl = eta * sin_t > 1.0f;
         if (!refl) {
             float r0 = (1.0f - eta) / (1.0f + eta);
             r0 = r0 * r0;
-            float rf = r0 + (1.0f - r0) * g_pow5(1.0f - cos_t);
-            refl = rf > rnd(g);
+            float rr = r0 + (1.0f - r0) * g_pow5(1.0f - cos_t);
+            refl = rr > rnd(rf, px, py);
         }
-        d = refl ? g_reflect(d, rec.normal) : g_refract(d, rec.normal, eta);
+        d = refl ? g_reflect(d, normal) : g_refract(d, normal, eta);
         should = true;
         skip_pdf = true;
     } else if (mid == RT_MAT_ISOTROPIC) {
-        d = rand_unit_vec(g);
+        d = rand_unit_vec(rf, px, py);
         should = true;
     }
-    if ((fabsf(d.x) < 1e-8f) && (fabsf(d.y) < 1e-8f) && (fabsf(d.z) < 1e-8f)) d = rec.normal;
+    if ((fabsf(d.x) < 1e-8f) && (fabsf(d.y) < 1e-8f) && (fabsf(d.z) < 1e-8f)) d = normal;
     if (!should) {
         result = mul3(S.acc, emis);
         return true;
     }
-    S.o = rec.p;
+    S.o = p;
     if (skip_pdf) {
-        S.acc = mul3(S.acc, texture_color(P, rec.p, tex_id, S.uvs, S.time));
+        S.acc = mul3(S.acc, texture_color(P, p, tex_id, S.uvs, S.time));
         S.d = d;
         return false;
     }
-    if (rnd(g) < 0.5f) d = lights_random(P, S.o, g);
-    float lpdf = (P.lights_count > 0) ? lights_pdf_value(P, S.o, d, S.time) : 0.0f;
+    if (rnd(rf, px, py) < 0.5f) d = lights_random(P, p, rf, px, py);
+    float lpdf = (P.lights_count > 0) ? lights_pdf_value(P, p, d, S.time) : 0.0f;
     float mpdf;
-    if (mid == RT_MAT_LAMBERTIAN) mpdf = g_max(0.0f, g_normalize1(g_dot(d, rec.normal)) / RT_PI);
+    if (mid == RT_MAT_LAMBERTIAN) mpdf = g_max(0.0f, g_normalize1(g_dot(d, normal)) / RT_PI);
     else if (mid == RT_MAT_ISOTROPIC) mpdf = 1.0f / (4.0f * RT_PI);
     else mpdf = 0.0f;
     float pdf = 0.5f * lpdf + 0.5f * mpdf;
@@ -621,30 +692,66 @@ __device__ __forceinline__ bool bounce(const KP& P, Path& S, v3& result) {
         return true;
     }
     float spdf;
-    if (mid == RT_MAT_LAMBERTIAN) spdf = g_max(0.0f, g_dot(rec.normal, g_normalize(d)) / RT_PI);
+    if (mid == RT_MAT_LAMBERTIAN) spdf = g_max(0.0f, g_dot(normal, g_normalize(d)) / RT_PI);
     else if (mid == RT_MAT_ISOTROPIC) spdf = 1.0f / (4.0f * RT_PI);
     else spdf = 0.0f;
-    v3 att = texture_color(P, rec.p, tex_id, S.uvs, S.time);
+    v3 att = texture_color(P, p, tex_id, S.uvs, S.time);
     S.acc = mul3(S.acc, divs3(scale3(att, spdf), pdf));
     S.d = d;
     return false;
 }
 
+// One iteration of ray_color's loop (compute.glsl:304-340).
+template <bool WW, bool STATS>
+__device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, Path& S, float px, float py,
+                                       v3& result, unsigned long long* st) {
+    if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
+        result = mk3s(0.0f);
+        return true;
+    }
+    S.depth++;
+    v3 d = S.d;
+    Hit h;
+    h.t = 0.0f; h.type = 0; h.idx = 0; h.face = 0;
+    h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
+    // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
+    bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
+    bool hit = !dir_zero && trace<WW, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+    unsigned long long ts = STATS ? clock64() : 0;
+    if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
+    // hit_record.uv as left by this walk (compute.glsl:62)
+    if (h.uv_kind_idx != 0) {
+        bool sph = (h.uv_kind_idx >> 16) == 1;
+        v3 up = add3(S.o, scale3(d, h.uv_a));   // the sphere hit's p (hitting.glsl:39)
+        S.uvs.kind_idx = h.uv_kind_idx;
+        S.uvs.a = sph ? up.x : h.uv_a;
+        S.uvs.b = sph ? up.y : h.uv_b;
+        S.uvs.c = sph ? up.z : S.uvs.c;
+    }
+    bool done;
+    if (!hit) {
+        result = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
+        done = true;
+    } else {
+        done = shade(P, S, h, px, py, result);
+    }
+    if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
+    return done;
+}
+
 // Camera ray of frame `frame_count` (compute.glsl:345-350, random.glsl:19-30,82-100).
-__device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count, float rf, float fx, float fy, v3 base) {
+__device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count, float rf0, float fx, float fy,
+                                           v3 base) {
     const rt_camera_ubo& C = P.cam;
     v3 du = ld3(C.pixel_delta_u), dv = ld3(C.pixel_delta_v), cpos = ld3(C.camera_pos);
-    Rng& g = S.g;
-    g.rf = rf;
-    g.px = fx;
-    g.py = fy;
-    S.time = rnd(g);
+    float rf = rf0;
+    S.time = rnd(rf, fx, fy);
     float col = g_mod((float)frame_count, P.sqrt_spp);
     float layer = (float)frame_count / P.sqrt_spp;
     float base_x = (col + 0.5f) * P.recip_sqrt_spp;
     float base_y = (layer + 0.5f) * P.recip_sqrt_spp;
-    float jx = (rnd(g) - 0.5f) * P.recip_sqrt_spp;
-    float jy = (rnd(g) - 0.5f) * P.recip_sqrt_spp;
+    float jx = (rnd(rf, fx, fy) - 0.5f) * P.recip_sqrt_spp;
+    float jy = (rnd(rf, fx, fy) - 0.5f) * P.recip_sqrt_spp;
     float spx = base_x + jx - 0.5f;
     float spy = base_y + jy - 0.5f;
     v3 coord = add3(base, add3(scale3(du, spx), scale3(dv, spy)));
@@ -652,31 +759,28 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
     if (!(C.defocus_angle <= 0.0f)) {
         float dx, dy;
         for (;;) {
-            dx = -1.0f + rnd(g) * 2.0f;
-            dy = -1.0f + rnd(g) * 2.0f;
+            dx = -1.0f + rnd(rf, fx, fy) * 2.0f;
+            dy = -1.0f + rnd(rf, fx, fy) * 2.0f;
             v3 p = mk3(dx, dy, 0.0f);
             if (g_dot(p, p) < 1.0f) break;
         }
         o = add3(add3(cpos, scale3(ld3(C.defocus_disk_u), dx)), scale3(ld3(C.defocus_disk_v), dy));
     }
+    S.rf = rf;
     S.o = o;
     S.d = sub3(coord, o);
     S.acc = mk3s(1.0f);
     S.depth = 0;
-    S.rec.t = 0.0f; S.rec.p = mk3s(0.0f); S.rec.normal = mk3s(0.0f); S.rec.front = false;
-    S.uvs.kind = 0; S.uvs.idx = 0; S.uvs.p = mk3s(0.0f); S.uvs.ab.x = 0.0f; S.uvs.ab.y = 0.0f;
+    S.uvs.kind_idx = 0; S.uvs.a = 0.0f; S.uvs.b = 0.0f; S.uvs.c = 0.0f;
 }
 
-// compute.glsl:345-358 for all frames of the launch.  Path regeneration: a lane
-// whose path ended starts its next frame at once, so a wave never idles until
-// its longest path of a frame is done; each pixel still runs its frames in order
-// and applies the running mean per frame.
-template <bool WW, int MINW>
-__global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict__ Pp) {
-    const KP& P = *Pp;
-    int x = blockIdx.x * 16 + threadIdx.x;
-    int lr = blockIdx.y * 16 + threadIdx.y;
-    if (x >= P.width || lr >= P.local_rows) return;
+// compute.glsl:345-358 for all frames of the launch, for the pixel at
+// column x of local (stripe-compacted) row lr.  Path regeneration: a lane whose
+// path ended starts its next frame at once; each pixel still runs its frames
+// in order and applies the running mean per frame.
+template <bool WW, bool STATS>
+__device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, int x, int lr,
+                                             unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
     int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
     float4* px = reinterpret_cast<float4*>(P.image) + (size_t)lr * P.width + x;
@@ -691,11 +795,14 @@ __global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict_
     for (;;) {
         if (fresh) {
             if (f >= P.n_frames) break;
+            unsigned long long t0 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
             start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, base);
+            if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
             fresh = false;
         }
         v3 cur;
-        if (bounce<WW>(P, S, cur)) {
+        if (bounce<WW, STATS>(P, nodes, S, fx, fy, cur, st)) {
             int fc = P.first_frame + f;
             float n1 = (float)(fc - 1), n = (float)fc;
             prev.x = (prev.x * n1 + cur.x) / n;
@@ -707,6 +814,85 @@ __global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict_
         }
     }
     *px = prev;
+}
+
+// Grid-per-image variant (A/B reference): 16x16 workgroups, one pixel each.
+template <bool WW, int MINW, bool STATS>
+__global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict__ Pp) {
+    const KP& P = *Pp;
+    __shared__ unsigned long long s_stats[STATS ? 4 : 1][STATS ? ST_N : 1];
+    unsigned long long* st = nullptr;
+    unsigned long long t_begin = 0;
+    int tid = threadIdx.y * 16 + threadIdx.x;
+    if (STATS) {
+        for (int k = tid; k < 4 * ST_N; k += 256) (&s_stats[0][0])[k] = 0;
+        __syncthreads();
+        st = s_stats[tid / 64];
+        t_begin = clock64();
+    }
+    int x = blockIdx.x * 16 + threadIdx.x;
+    int lr = blockIdx.y * 16 + threadIdx.y;
+    bool active = x < P.width && lr < P.local_rows;
+    if (!STATS && !active) return;
+    if (active) render_pixel<WW, STATS>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, st);
+    if (STATS) {
+        st_add(st, ST_TOTAL, clock64() - t_begin);
+        __syncthreads();
+        if (tid < ST_N) {
+            unsigned long long v = 0;
+            for (int w = 0; w < 4; w++) v += s_stats[w][tid];
+            atomicAdd(P.stats + tid, v);
+        }
+    }
+}
+
+// Persistent variant (default): one resident grid; each workgroup stages the
+// threaded BVH (32 B/node, 57 KB for scene 8) in LDS once, then each wave
+// repeatedly takes the next 8x8 pixel tile from a device-wide counter (one
+// returning atomic per tile) until the counter passes the last tile — a
+// condition every wave reaches.
+template <bool WW, int MINW, bool STATS, bool LDSN, int BLOCK>
+__global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
+    const KP& P = *Pp;
+    extern __shared__ float4 s_nodes[];
+    __shared__ unsigned long long s_stats[STATS ? BLOCK / 64 : 1][STATS ? ST_N : 1];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    unsigned long long* st = nullptr;
+    unsigned long long t_begin = 0;
+    if (STATS) {
+        for (int k = tid; k < (BLOCK / 64) * ST_N; k += BLOCK) (&s_stats[0][0])[k] = 0;
+        st = s_stats[tid / 64];
+    }
+    if (LDSN) {
+        const float4* g = reinterpret_cast<const float4*>(P.nodes);
+        for (int k = tid; k < 2 * P.n_nodes; k += BLOCK) s_nodes[k] = g[k];
+    }
+    if (LDSN || STATS) __syncthreads();
+    if (STATS) t_begin = clock64();
+    const int tiles_x = (P.width + 7) >> 3;
+    const int n_tiles = tiles_x * ((P.local_rows + 7) >> 3);
+    for (;;) {
+        int tile = 0;
+        if (lane == 0) tile = atomicAdd(P.tile_counter, 1);
+        tile = __shfl(tile, 0);
+        if (tile >= n_tiles) break;
+        int x = (tile % tiles_x) * 8 + (lane & 7);
+        int lr = (tile / tiles_x) * 8 + (lane >> 3);
+        if (x < P.width && lr < P.local_rows) {
+            if (LDSN) render_pixel<WW, STATS>(P, s_nodes, x, lr, st);
+            else render_pixel<WW, STATS>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, st);
+        }
+    }
+    if (STATS) {
+        st_add(st, ST_TOTAL, clock64() - t_begin);
+        __syncthreads();
+        if (tid < ST_N) {
+            unsigned long long v = 0;
+            for (int w = 0; w < BLOCK / 64; w++) v += s_stats[w][tid];
+            atomicAdd(P.stats + tid, v);
+        }
+    }
 }
 
 __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const float* __restrict__ y,
@@ -727,32 +913,67 @@ __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const f
     out[i] = r;
 }
 
+template <typename K>
+int launch_persistent(K kernel, int block, size_t lds, const rt_kernel_args* d, hipStream_t st) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    hipLaunchKernelGGL(kernel, dim3(cus * per_cu), dim3(block), lds, st, d);
+    return 0;
+}
+
 }  // namespace
 
 int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.
-    // Same-stream ordering makes one slot per device safe to reuse per launch.
-    if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess) return -1;
+    // `a` is a pinned staging slot; same-stream ordering makes one device slot
+    // safe to reuse per launch.
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
+    const rt_kernel_args* d = (const rt_kernel_args*)dargs;
+    // Variants (A/B only; all bit-identical):
+    //   persistent (default 0 = 10): 10 WW/512/4w, 11 WW/640/5w, 12 WW/512/4w global nodes,
+    //                                14 if-if/512/4w, 19 stats of 10
+    //   grid per image: 1 if-if, 2 WW 4w, 3 WW 5w, 4 if-if 4w, 5 WW default, 9 stats of 5
+    if (a.variant == 0 || a.variant >= 10) {
+        if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
+        size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
+        bool fits = lds <= RT_LDS_NODE_BYTES;
+        int rc;
+        switch (a.variant) {
+            case 11: rc = fits ? launch_persistent(render_persistent<true, 5, false, true, 640>, 640, lds, d, st)
+                               : launch_persistent(render_persistent<true, 5, false, false, 640>, 640, 0, d, st); break;
+            case 12: rc = launch_persistent(render_persistent<true, 4, false, false, 512>, 512, 0, d, st); break;
+            case 14: rc = fits ? launch_persistent(render_persistent<false, 4, false, true, 512>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<false, 4, false, false, 512>, 512, 0, d, st); break;
+            case 19: rc = fits ? launch_persistent(render_persistent<true, 4, true, true, 512>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<true, 4, true, false, 512>, 512, 0, d, st); break;
+            default: rc = fits ? launch_persistent(render_persistent<true, 4, false, true, 512>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<true, 4, false, false, 512>, 512, 0, d, st); break;
+        }
+        if (rc) return rc;
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     dim3 block(16, 16);
     dim3 grid((a.width + 15) / 16, (a.local_rows + 15) / 16);
-    // variant (A/B only): 0 while-while default occupancy, 1 if-if, 2/3 while-while
-    // with >= 4 / >= 5 waves per SIMD, 4 if-if with >= 4 waves per SIMD.
-    const rt_kernel_args* d = (const rt_kernel_args*)dargs;
-    hipStream_t st = (hipStream_t)stream;
     switch (a.variant) {
-        case 1: hipLaunchKernelGGL((render_kernel<false, 1>), grid, block, 0, st, d); break;
-        case 2: hipLaunchKernelGGL((render_kernel<true, 4>), grid, block, 0, st, d); break;
-        case 3: hipLaunchKernelGGL((render_kernel<true, 5>), grid, block, 0, st, d); break;
-        case 4: hipLaunchKernelGGL((render_kernel<false, 4>), grid, block, 0, st, d); break;
-        default: hipLaunchKernelGGL((render_kernel<true, 1>), grid, block, 0, st, d); break;
+        case 1: hipLaunchKernelGGL((render_kernel<false, 1, false>), grid, block, 0, st, d); break;
+        case 2: hipLaunchKernelGGL((render_kernel<true, 4, false>), grid, block, 0, st, d); break;
+        case 3: hipLaunchKernelGGL((render_kernel<true, 5, false>), grid, block, 0, st, d); break;
+        case 4: hipLaunchKernelGGL((render_kernel<false, 4, false>), grid, block, 0, st, d); break;
+        case 9: hipLaunchKernelGGL((render_kernel<true, 1, true>), grid, block, 0, st, d); break;
+        default: hipLaunchKernelGGL((render_kernel<true, 1, false>), grid, block, 0, st, d); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(eval_builtin_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, dx, dy, dout, n);
+    hipLaunchKernelGGL(eval_builtin_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, dx, dy, dout,
+                       n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

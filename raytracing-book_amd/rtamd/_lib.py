@@ -83,6 +83,8 @@ def amd():
         _proto(L, "rt_debug_eval_builtin", i, i, i, c_float_p, c_float_p, c_float_p, i)
         _proto(L, "rt_debug_threaded_bvh", i, vp, sz, vp, sz, c_int_p)
         _proto(L, "rt_debug_device_count", i)
+        _proto(L, "rt_debug_enable_stats", i, vp, i)
+        _proto(L, "rt_debug_read_stats", i, vp, ctypes.POINTER(ctypes.c_ulonglong), i)
         _amd = L
     return _amd
 

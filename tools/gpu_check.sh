@@ -22,6 +22,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     ab)    run ab 600 python tools/ab_variants.py ${AB_ARGS:-} ;;
+    stats) run kstats 300 python tools/kernel_stats.py ${STATS_ARGS:-} ;;
     list)  run pmc_list 120 rocprofv3 -L ;;
     pmc)   run pmc 900 python tools/pmc_profile.py ${PMC_ARGS:-} ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;

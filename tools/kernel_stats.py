@@ -1,0 +1,53 @@
+"""Run the diagnostic stats build of the render kernel and print where wave time
+goes (s_memtime per region, once per wave) and each region's SIMD lane use.
+usage: python tools/kernel_stats.py [--scene 8] [--frames 16] [--width 1920 --height 1080]"""
+import argparse
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracing-book_amd"))
+import rtamd  # noqa: E402
+
+NAMES = ["TOTAL", "START_CYC", "START_IT", "START_LN", "NODE_CYC", "NODE_IT", "NODE_LN", "LEAF_CYC", "LEAF_IT",
+         "LEAF_LN", "SPH_LN", "QUAD_LN", "BOX_LN", "MED_LN", "SHADE_CYC", "SHADE_IT", "SHADE_LN", "SPH_IT",
+         "QUAD_IT", "BOX_IT", "MED_IT"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", type=int, default=8)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--depth", type=int, default=5)
+    a = ap.parse_args()
+    scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
+    ctx = rtamd.RenderContext(devices=(0,))
+    ctx.upload_scene(scene)
+    ctx.set_params(max_depth=a.depth, spp=4096)
+    ctx.resize(a.width, a.height)
+    L = rtamd.amd()
+    assert L.rt_debug_enable_stats(ctx._h, 1) == 0
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, a.frames))
+    ctx.sync()
+    buf = (ctypes.c_ulonglong * 64)()
+    assert L.rt_debug_read_stats(ctx._h, buf, 64) == 0
+    v = {n: buf[i] for i, n in enumerate(NAMES)}
+    tot = v["TOTAL"] or 1
+    samples = a.width * a.height * a.frames
+    print(f"scene {a.scene} {a.width}x{a.height}x{a.frames}: {samples} samples, wave-cycles total {tot:.3e}")
+    for reg in ["START", "NODE", "LEAF", "SHADE"]:
+        cyc, it, ln = v[reg + "_CYC"], v[reg + "_IT"], v[reg + "_LN"]
+        util = ln / (64.0 * it) if it else 0
+        print(f"  {reg:6s} {100.0 * cyc / tot:5.1f}% of wave-cycles  iterations {it:.3e}  lane-util {100 * util:5.1f}%  "
+              f"cyc/iter {cyc / max(it, 1):7.1f}  lane-iters/sample {ln / samples:6.2f}")
+    for t in ["SPH", "QUAD", "BOX", "MED"]:
+        it, ln = v[t + "_IT"], v[t + "_LN"]
+        print(f"  leaf-slot {t:4s}: wave-executions {it:.3e} lanes/exec {ln / max(it, 1):5.2f}  per-sample {ln / samples:5.2f}")
+    print("raw", v)
+
+
+if __name__ == "__main__":
+    main()
