@@ -66,6 +66,14 @@ struct Counters {
     Counters() { std::memset(&c, 0, sizeof(c)); }
 };
 
+// Optional traversal log (analysis only): node indices visited per trace.
+struct TraceLog {
+    std::vector<int32_t>* out = nullptr;   // records: [pixel, frame, bounce, n, nodes...]
+    int pixel = 0, frame = 0, bounce = 0;
+    std::vector<int32_t> cur;
+};
+thread_local TraceLog* g_tlog = nullptr;
+
 // ------------------------------------------------------- GLSL structs
 struct Ray { v3 o, dir; };
 struct HitRecord { bool is_front_face = false; v3 p = mk3s(0); v3 normal = mk3s(0); float t = 0; v2 uv = {0, 0}; };
@@ -646,9 +654,11 @@ bool trace_through_bvh(Inv& I, const Ray& ray, Interval ray_t, HitRecord& rec) {
     int sp = 0;
     stack[sp++] = 0;
     bool has_hit = false;
+    if (g_tlog) g_tlog->cur.clear();
     while (sp > 0) {
         int node_idx = stack[--sp];
         const rt_bvh_node& node = S.nodes[node_idx];
+        if (g_tlog) g_tlog->cur.push_back(node_idx);
         if (I.C) { I.C->c.node_visits++; I.C->c.node_bytes += 32; }
         if (hit_aabb(ray, ray_t, node)) {
             int node_type = node.left_id & 0xFFFF;
@@ -669,6 +679,13 @@ bool trace_through_bvh(Inv& I, const Ray& ray, Interval ray_t, HitRecord& rec) {
                 stack[sp++] = (node.right_id >> 16) & 0xFFFF;
             }
         }
+    }
+    if (g_tlog) {
+        std::vector<int32_t>& o = *g_tlog->out;
+        o.push_back(g_tlog->pixel); o.push_back(g_tlog->frame); o.push_back(g_tlog->bounce);
+        o.push_back((int32_t)g_tlog->cur.size());
+        o.insert(o.end(), g_tlog->cur.begin(), g_tlog->cur.end());
+        g_tlog->bounce++;
     }
     return has_hit;
 }
@@ -808,6 +825,31 @@ int oracle_render(const oracle_scene_desc* d, int width, int height, float* rgba
         }
     }
     return 0;
+}
+
+// Analysis hook: render rows [y0, y1) x cols [x0, x1), frames, logging each
+// trace's node sequence (pixel = y*W + x).  Returns the number of int32 written.
+long oracle_trace_log(const oracle_scene_desc* d, int width, int height, int x0, int x1, int y0, int y1,
+                      int first_frame, int n_frames, const float* rand_factors, int32_t* out, long cap) {
+    Scene S;
+    if (!make_scene(d, S)) return -1;
+    std::vector<int32_t> buf;
+    TraceLog L;
+    L.out = &buf;
+    g_tlog = &L;
+    std::vector<float> px(4);
+    for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++) {
+            px[0] = px[1] = px[2] = px[3] = 0.0f;
+            for (int f = 0; f < n_frames; f++) {
+                L.pixel = y * width + x; L.frame = f; L.bounce = 0;
+                shade_pixel(S, nullptr, x, y, first_frame + f, rand_factors[f], px.data());
+            }
+        }
+    g_tlog = nullptr;
+    long n = (long)buf.size();
+    if (out && n <= cap) std::memcpy(out, buf.data(), n * 4);
+    return n;
 }
 
 void oracle_get_sphere_uv(float x, float y, float z, float* u, float* v) {

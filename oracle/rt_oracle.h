@@ -61,6 +61,11 @@ int oracle_render(const oracle_scene_desc* d, int width, int height, float* rgba
                   int rank, int world, int stripe_rows, int nthreads,
                   oracle_counters* counters);
 
+/* Analysis hook: per-trace BVH node sequences for a pixel window
+ * (records [pixel, frame, bounce, n, node...]); returns int32 count. */
+long oracle_trace_log(const oracle_scene_desc* d, int width, int height, int x0, int x1, int y0, int y1,
+                      int first_frame, int n_frames, const float* rand_factors, int32_t* out, long cap);
+
 /* Known-answer hooks. */
 void oracle_get_sphere_uv(float x, float y, float z, float* u, float* v);
 /* n successive rand() values for an invocation at (px,py) with u_rand_factor f */

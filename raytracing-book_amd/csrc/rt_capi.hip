@@ -702,7 +702,7 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
         if (d.stats.ptr) HIPCHK(c, hipMemsetAsync(d.stats.ptr, 0, d.stats.bytes, d.stream));
         HIPCHK(c, hipStreamSynchronize(d.stream));
     }
-    c->variant = on ? ((c->variant == 0 || c->variant >= 10) ? 19 : 9) : 0;
+    c->variant = on ? ((c->variant >= 20) ? 29 : ((c->variant == 0 || c->variant >= 10) ? 19 : 9)) : 0;
     return RT_OK;
 }
 

@@ -346,6 +346,64 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
     return has;
 }
 
+// Minimum over the 64 lanes (DPP row shifts + row broadcasts); EXEC must be full.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    const int ID = (int)0xFFFFFFFFu;
+    uint32_t x = v, y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x111, 0xf, 0xf, false); x = y < x ? y : x;   // row_shr:1
+    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x112, 0xf, 0xf, false); x = y < x ? y : x;   // row_shr:2
+    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x114, 0xf, 0xf, false); x = y < x ? y : x;   // row_shr:4
+    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x118, 0xf, 0xf, false); x = y < x ? y : x;   // row_shr:8
+    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x142, 0xa, 0xf, false); x = y < x ? y : x;   // row_bcast:15
+    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x143, 0xc, 0xf, false); x = y < x ? y : x;   // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// compute.glsl:226-266, wave-uniform schedule.  Every lane's visit sequence is
+// an increasing subsequence of the right-first pre-order array, so the wave
+// walks node i = min over lanes of next[lane]: lanes with next == i take their
+// reference step (AABB test; inner hit -> i+1, leaf hit -> its two prims, miss
+// or leaf done -> skip) and the others wait.  Each lane's node order, ray_t
+// updates and rand() draws are exactly its own reference sequence; the node
+// record is a broadcast read and a leaf's prim type/index are wave-uniform.
+// Called by all 64 lanes (EXEC full); lanes with want == false do not walk.
+template <bool STATS>
+__device__ __forceinline__ bool trace_uniform(const KP& P, const float4* __restrict__ nodes, bool want, v3 o, v3 d,
+                                              float time, float& rf, float px, float py, Hit& h,
+                                              unsigned long long* st) {
+    uint32_t n = (want && P.n_nodes > 0) ? 0u : RT_NODE_END;
+    float tmin = 0.001f, tmax = RT_INFINITY;
+    v3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float a = g_dot(d, d);
+    bool has = false;
+    uint32_t i = wave_min_u32(n);
+    unsigned long long t0 = STATS ? clock64() : 0;
+    while (i != RT_NODE_END) {
+        float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
+        uint32_t meta = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(n1.z));
+        uint32_t prims = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(n1.w));
+        uint32_t skip = meta & 0xFFFFu;
+        bool is_leaf = ((meta >> 16) & 0xFu) != 0;
+        bool part = (n == i);
+        if (STATS) st_pred(st, part, ST_NODE_IT, ST_NODE_LN);
+        float lo = tmin, hi = tmax;
+        slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+        slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+        slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+        bool hitb = part && !(hi <= lo);
+        if (part) n = (hitb && !is_leaf) ? i + 1 : skip;
+        if (is_leaf && __ballot(hitb) != 0) {
+            unsigned long long t1 = STATS ? clock64() : 0;
+            if (STATS) st_pred(st, hitb, ST_LEAF_IT, ST_LEAF_LN);
+            if (hitb) leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+        }
+        i = (__ballot(n == i + 1) != 0) ? i + 1 : wave_min_u32(n);
+    }
+    if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
+    return has;
+}
+
 // ---------------------------------------------------------------- textures
 __device__ __forceinline__ void texel(const rt_dtex& T, int x, int y, float out[3]) {
     out[0] = out[1] = out[2] = 0.0f;
@@ -816,6 +874,76 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
     *px = prev;
 }
 
+// ray_color for a whole wave with the wave-uniform walk: frames run in
+// lock-step per wave (no regeneration), so each bounce's walk is shared by the
+// lanes still alive.  Called by all 64 lanes; `valid` lanes own a pixel.
+template <bool STATS>
+__device__ __forceinline__ void render_pixel_uniform(const KP& P, const float4* __restrict__ nodes, int x, int lr,
+                                                     bool valid, unsigned long long* st) {
+    int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
+    int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
+    float4* px = reinterpret_cast<float4*>(P.image) + ((size_t)lr * P.width + x);
+    float4 prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (valid) prev = *px;
+    const rt_camera_ubo& C = P.cam;
+    float fx = (float)x, fy = (float)y;
+    v3 base = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
+    Path S;
+    S.o = mk3s(0.0f); S.d = mk3s(0.0f); S.acc = mk3s(0.0f); S.time = 0.0f; S.rf = 0.0f; S.depth = 0;
+    S.uvs.kind_idx = 0; S.uvs.a = 0.0f; S.uvs.b = 0.0f; S.uvs.c = 0.0f;
+    for (int f = 0; f < P.n_frames; f++) {
+        if (valid) {
+            unsigned long long t0 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
+            start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, base);
+            if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
+        }
+        bool alive = valid;
+        v3 cur = mk3s(0.0f);
+        while (__ballot(alive) != 0) {
+            // compute.glsl:304 loop bound; final_color stays vec3(0) when exhausted
+            if (alive && S.depth >= P.max_depth) { cur = mk3s(0.0f); alive = false; }
+            bool go = alive;
+            if (go) S.depth++;
+            v3 d = S.d;
+            // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
+            bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
+            Hit h;
+            h.t = 0.0f; h.type = 0; h.idx = 0; h.face = 0;
+            h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
+            bool hit = trace_uniform<STATS>(P, nodes, go && !dir_zero, S.o, d, S.time, S.rf, fx, fy, h, st);
+            if (go) {
+                unsigned long long ts = STATS ? clock64() : 0;
+                if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
+                if (h.uv_kind_idx != 0) {
+                    bool sph = (h.uv_kind_idx >> 16) == 1;
+                    v3 up = add3(S.o, scale3(d, h.uv_a));
+                    S.uvs.kind_idx = h.uv_kind_idx;
+                    S.uvs.a = sph ? up.x : h.uv_a;
+                    S.uvs.b = sph ? up.y : h.uv_b;
+                    S.uvs.c = sph ? up.z : S.uvs.c;
+                }
+                if (!hit) {
+                    cur = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
+                    alive = false;
+                } else if (shade(P, S, h, fx, fy, cur)) {
+                    alive = false;
+                }
+                if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
+            }
+        }
+        if (valid) {
+            int fc = P.first_frame + f;
+            float n1 = (float)(fc - 1), nn = (float)fc;
+            prev.x = (prev.x * n1 + cur.x) / nn;
+            prev.y = (prev.y * n1 + cur.y) / nn;
+            prev.z = (prev.z * n1 + cur.z) / nn;
+            prev.w = 1.0f;
+        }
+    }
+    if (valid) *px = prev;
+}
+
 // Grid-per-image variant (A/B reference): 16x16 workgroups, one pixel each.
 template <bool WW, int MINW, bool STATS>
 __global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict__ Pp) {
@@ -851,7 +979,7 @@ __global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict_
 // repeatedly takes the next 8x8 pixel tile from a device-wide counter (one
 // returning atomic per tile) until the counter passes the last tile — a
 // condition every wave reaches.
-template <bool WW, int MINW, bool STATS, bool LDSN, int BLOCK>
+template <bool WW, int MINW, bool STATS, bool LDSN, int BLOCK, bool UNI = false>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
@@ -879,7 +1007,13 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         if (tile >= n_tiles) break;
         int x = (tile % tiles_x) * 8 + (lane & 7);
         int lr = (tile / tiles_x) * 8 + (lane >> 3);
-        if (x < P.width && lr < P.local_rows) {
+        bool valid = x < P.width && lr < P.local_rows;
+        if (UNI) {
+            // every lane enters (EXEC stays full for the wave-uniform walk)
+            int xc = valid ? x : 0, lc = valid ? lr : 0;
+            if (LDSN) render_pixel_uniform<STATS>(P, s_nodes, xc, lc, valid, st);
+            else render_pixel_uniform<STATS>(P, reinterpret_cast<const float4*>(P.nodes), xc, lc, valid, st);
+        } else if (valid) {
             if (LDSN) render_pixel<WW, STATS>(P, s_nodes, x, lr, st);
             else render_pixel<WW, STATS>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, st);
         }
@@ -952,6 +1086,15 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
                                : launch_persistent(render_persistent<false, 4, false, false, 512>, 512, 0, d, st); break;
             case 19: rc = fits ? launch_persistent(render_persistent<true, 4, true, true, 512>, 512, lds, d, st)
                                : launch_persistent(render_persistent<true, 4, true, false, 512>, 512, 0, d, st); break;
+            case 20: rc = fits ? launch_persistent(render_persistent<true, 4, false, true, 512, true>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<true, 4, false, false, 512, true>, 512, 0, d, st); break;
+            case 21: rc = launch_persistent(render_persistent<true, 4, false, false, 512, true>, 512, 0, d, st); break;
+            case 22: rc = fits ? launch_persistent(render_persistent<true, 1, false, true, 512, true>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<true, 1, false, false, 512, true>, 512, 0, d, st); break;
+            case 23: rc = fits ? launch_persistent(render_persistent<true, 4, false, true, 1024, true>, 1024, lds, d, st)
+                               : launch_persistent(render_persistent<true, 4, false, false, 1024, true>, 1024, 0, d, st); break;
+            case 29: rc = fits ? launch_persistent(render_persistent<true, 4, true, true, 512, true>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<true, 4, true, false, 512, true>, 512, 0, d, st); break;
             default: rc = fits ? launch_persistent(render_persistent<true, 4, false, true, 512>, 512, lds, d, st)
                                : launch_persistent(render_persistent<true, 4, false, false, 512>, 512, 0, d, st); break;
         }

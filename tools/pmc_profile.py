@@ -23,6 +23,8 @@ GROUPS = [
     ["TCC_HIT_sum", "TCC_MISS_sum"],
     ["TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum"],
     ["GRBM_GUI_ACTIVE", "GRBM_COUNT"],
+    ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_SCRATCH" if False else "SQ_INSTS_FLAT"],
+    ["SQ_WAIT_INST_LDS", "SQ_INSTS_BRANCH", "SQ_INST_CYCLES_VMEM", "SQ_ACTIVE_INST_SCA"],
 ]
 
 
@@ -60,7 +62,7 @@ def main():
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
-                    if "render_kernel" not in row.get("Kernel_Name", ""):
+                    if "render_" not in row.get("Kernel_Name", ""):
                         continue
                     name = row.get("Counter_Name")
                     val = float(row.get("Counter_Value", 0))
