@@ -50,6 +50,8 @@ typedef struct rt_ctx rt_ctx;
  * Replaces: Window.initGLFW/initShaderPrograms (Window.java:90-193). */
 int rt_create(int n_devices, const int* device_ids, rt_ctx** out);
 int rt_destroy(rt_ctx* ctx);
+/* Message of the last failure on ctx; with ctx == NULL, of the last failed
+ * rt_create on the calling thread. */
 const char* rt_last_error(rt_ctx* ctx);
 int rt_abi_version(void);
 

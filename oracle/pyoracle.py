@@ -110,6 +110,8 @@ def render(oscene, rand_factors, first_frame=1, image=None, rank=0, world=1, str
     W, H = oscene.width, oscene.height
     if image is None:
         image = np.zeros((H, W, 4), dtype=np.float32)
+    if image.shape != (H, W, 4) or image.dtype != np.float32 or not image.flags.c_contiguous:
+        raise ValueError(f"oracle image must be a contiguous float32 [{H}, {W}, 4] array (full size, any rank)")
     rf = np.ascontiguousarray(rand_factors, dtype=np.float32)
     cnt = OracleCounters() if counters else None
     rc = L.oracle_render(ctypes.byref(oscene.desc), W, H, _fp(image), int(first_frame), int(rf.size), _fp(rf),

@@ -280,27 +280,32 @@ extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
+// Failure of the last context-less call (rt_create) on this thread; rt_last_error(NULL).
+namespace { thread_local std::string g_create_err; }
+
 int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
-    if (!out) return RT_ERR_INVALID_ARG;
+    auto fail = [](int code, const char* msg) { g_create_err = msg; return code; };
+    if (!out) return fail(RT_ERR_INVALID_ARG, "rt_create: NULL out");
     *out = nullptr;
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RT_ERR_DEVICE;
-    if (n_devices <= 0 || n_devices > count) return RT_ERR_INVALID_ARG;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(RT_ERR_DEVICE, "rt_create: no HIP device");
+    if (n_devices <= 0 || n_devices > count) return fail(RT_ERR_INVALID_ARG, "rt_create: bad device count");
     rt_ctx* c = new rt_ctx();
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) c->variant = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
         Device& d = c->devs[i];
         d.id = device_ids ? device_ids[i] : i;
-        if (d.id < 0 || d.id >= count) { delete c; return RT_ERR_INVALID_ARG; }
+        if (d.id < 0 || d.id >= count) { delete c; return fail(RT_ERR_INVALID_ARG, "rt_create: device id out of range"); }
         d.rank = i;
         d.world = n_devices;
         if (hipSetDevice(d.id) != hipSuccess || hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreate(&d.ev_start) != hipSuccess || hipEventCreate(&d.ev_stop) != hipSuccess) {
             delete c;
-            return RT_ERR_DEVICE;
+            return fail(RT_ERR_DEVICE, "rt_create: stream/event creation failed");
         }
     }
+    g_create_err.clear();
     *out = c;
     return RT_OK;
 }
@@ -324,7 +329,7 @@ int rt_destroy(rt_ctx* c) {
     return RT_OK;
 }
 
-const char* rt_last_error(rt_ctx* c) { return c ? c->err.c_str() : "NULL context"; }
+const char* rt_last_error(rt_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
 int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
     if (!c) return RT_ERR_INVALID_ARG;

@@ -72,7 +72,7 @@ class RenderContext:
         h = ctypes.c_void_p()
         rc = L.rt_create(len(devices), devs, ctypes.byref(h))
         if rc != 0:
-            raise RTError(rc, "rt_create failed (no HIP device visible?)")
+            raise RTError(rc, L.rt_last_error(None).decode())
         self._h = h
         self.devices = tuple(devices)
         self.rank, self.world, self.stripe_rows = rank, world, stripe_rows
