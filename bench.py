@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--spp-total", type=int, default=4096, help="sqrt_spp uniform (BASELINE C3: 4096)")
     p.add_argument("--stripe-rows", type=int, default=16)
     p.add_argument("--seed", type=int, default=1)
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--png", default=None)
     return p.parse_args()
@@ -53,41 +53,49 @@ def parse():
 
 def cpu_baseline(scene, args):
     """CPU oracle (oracle/, the build's scalar restatement; the reference has no
-    CPU path) timed on the host: full-width rows of the same image (1 stripe in
-    8), frames scaled to ~cpu_seconds.  Also returns the oracle's logical
-    record-traffic count (bytes/sample) on a small sample of the same config."""
+    CPU path) timed on this host over a bounded sample of the same
+    workload: the full-width rows of stripe 0 of 8 (1/8 of the image), as many
+    frames as fit in ~cpu_seconds.  The rate does not depend on spp."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     import rtamd
-    threads = min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
     osc = pyoracle.OracleScene(scene, max_depth=args.depth, spp=args.spp_total)
     W, H = scene.width, scene.height
     world_s = 8
     rows = rtamd.local_rows(H, 0, world_s, args.stripe_rows)
-    # counted pass (bytes per sample), 1 frame
-    _, cnt = pyoracle.render(osc, rtamd.frame_rand_factors(args.seed, 0, 1), rank=0, world=world_s * 4,
-                             stripe_rows=args.stripe_rows, nthreads=threads, counters=True)
-    keys = ["framebuffer_bytes", "node_bytes", "prim_bytes", "material_bytes", "texel_bytes", "light_bytes"]
-    bytes_per_sample = sum(cnt[k] for k in keys) / max(1, cnt["samples"])
-    # timing pass
-    t = time.perf_counter()
-    pyoracle.render(osc, rtamd.frame_rand_factors(args.seed, 0, 1), rank=0, world=world_s,
-                    stripe_rows=args.stripe_rows, nthreads=threads)
-    t1 = time.perf_counter() - t
-    nf = max(1, min(64, int(args.cpu_seconds / max(t1, 1e-3))))
-    t = time.perf_counter()
-    pyoracle.render(osc, rtamd.frame_rand_factors(args.seed, 1, nf), first_frame=2, rank=0, world=world_s,
-                    stripe_rows=args.stripe_rows, nthreads=threads)
-    dt = time.perf_counter() - t
+    image = np.zeros((H, W, 4), np.float32)
+    # frames in growing chunks (progressive accumulation continues) until ~cpu_seconds
+    nf, chunk, dt = 0, 1, 0.0
+    while dt < args.cpu_seconds and nf < 65536:
+        rf = rtamd.frame_rand_factors(args.seed, nf, chunk)
+        t = time.perf_counter()
+        pyoracle.render(osc, rf, first_frame=nf + 1, image=image, rank=0, world=world_s,
+                        stripe_rows=args.stripe_rows, nthreads=threads)
+        dt += time.perf_counter() - t
+        nf += chunk
+        chunk = max(1, min(2 * chunk, int((args.cpu_seconds - dt) / (dt / nf)) if dt < args.cpu_seconds else 1))
     samples = W * rows * nf
     return {
-        "value": samples / dt / 1e6,
+        "value": round(samples / dt / 1e6, 3),
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"scene {args.scene} {W}x{H}, rows of stripe 0/{world_s} ({rows} rows), {nf} frames "
-                  f"(= {samples} samples, {dt:.1f} s), depth {args.depth}",
-    }, bytes_per_sample, cnt
+        "sample": f"scene {args.scene} {W}x{H} max_depth {args.depth}: rows of stripe 0/{world_s} "
+                  f"({rows} rows x {W}), {nf} frames = {samples} samples in {dt:.1f} s, "
+                  f"{threads} threads",
+    }
+
+
+def bytes_per_sample(args):
+    """Committed algorithmic bytes/sample (tools/count_bytes.py)."""
+    with open(os.path.join(REPO, "bench", "bytes_per_sample.json")) as f:
+        rec = json.load(f)[f"scene{args.scene}_depth{args.depth}"]
+    c = rec["config"]
+    if (c["width"], c["height"], c["seed"]) != (args.width, args.height, args.seed):
+        log("note: bytes_per_sample.json was counted for", c)
+    return rec["bytes_per_sample"]
 
 
 def main():
@@ -174,18 +182,16 @@ def main():
     nan_px = int(np.isnan(full[..., :3]).any(axis=-1).sum())
 
     cpu = None
-    bps = None
     if not args.no_cpu_baseline:
         try:
-            cpu, bps, _ = cpu_baseline(scene, args)
+            cpu = cpu_baseline(scene, args)
         except Exception as e:  # the baseline is reported, not required
             log("cpu baseline failed:", repr(e))
-    if bps is None:
-        try:
-            with open(os.path.join(REPO, "bench", "bytes_per_sample.json")) as f:
-                bps = json.load(f)[f"scene{args.scene}_depth{args.depth}"]["bytes_per_sample"]
-        except Exception:
-            bps = None
+    try:
+        bps = bytes_per_sample(args)
+    except (OSError, KeyError) as e:
+        log("no committed bytes/sample for this config:", repr(e))
+        bps = None
 
     avg_launch_ms = float(np.mean(kernel_ms)) / launches_per_step
     samples_per_launch = n_local_px * min(F, 256)
@@ -202,7 +208,7 @@ def main():
             pass
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "bytes_per_sample": round(bps, 1), "kernel": "render_kernel",
+                    "bytes_per_sample": round(bps, 1), "kernel": "render_persistent",
                     "avg_launch_ms": round(avg_launch_ms, 3), "samples_per_launch": samples_per_launch}
 
     out = {

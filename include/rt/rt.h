@@ -45,8 +45,9 @@ enum {
 typedef struct rt_ctx rt_ctx;
 
 /* Create a context rendering on n_devices HIP devices (device_ids may be NULL
- * for 0..n-1).  Rows are split in interleaved stripes over the devices; the
- * result equals a 1-device render bit for bit.
+ * for 0..n-1; explicit ids may repeat, n <= 64).  Rows are split in
+ * interleaved stripes over the device slots and gathered on the host by
+ * rt_read_image; the result equals a 1-device render bit for bit.
  * Replaces: Window.initGLFW/initShaderPrograms (Window.java:90-193). */
 int rt_create(int n_devices, const int* device_ids, rt_ctx** out);
 int rt_destroy(rt_ctx* ctx);

@@ -289,7 +289,9 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(RT_ERR_DEVICE, "rt_create: no HIP device");
-    if (n_devices <= 0 || n_devices > count) return fail(RT_ERR_INVALID_ARG, "rt_create: bad device count");
+    // Explicit ids may repeat (several stripe slots on one device); without ids, devices 0..n-1.
+    if (n_devices <= 0 || n_devices > 64 || (!device_ids && n_devices > count))
+        return fail(RT_ERR_INVALID_ARG, "rt_create: bad device count");
     rt_ctx* c = new rt_ctx();
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) c->variant = std::atoi(v);
     c->devs.resize(n_devices);

@@ -1071,7 +1071,8 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     const rt_kernel_args* d = (const rt_kernel_args*)dargs;
     // Variants (A/B only; all bit-identical):
     //   persistent (default 0 = 10): 10 WW/512/4w, 11 WW/640/5w, 12 WW/512/4w global nodes,
-    //                                14 if-if/512/4w, 19 stats of 10
+    //                                14 if-if/512/4w, 15 WW/768/3w, 16 WW/768/3w global nodes,
+    //                                17 WW/512/2w, 19 stats of 10
     //   grid per image: 1 if-if, 2 WW 4w, 3 WW 5w, 4 if-if 4w, 5 WW default, 9 stats of 5
     if (a.variant == 0 || a.variant >= 10) {
         if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
@@ -1082,6 +1083,11 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
             case 11: rc = fits ? launch_persistent(render_persistent<true, 5, false, true, 640>, 640, lds, d, st)
                                : launch_persistent(render_persistent<true, 5, false, false, 640>, 640, 0, d, st); break;
             case 12: rc = launch_persistent(render_persistent<true, 4, false, false, 512>, 512, 0, d, st); break;
+            case 15: rc = fits ? launch_persistent(render_persistent<true, 3, false, true, 768>, 768, lds, d, st)
+                               : launch_persistent(render_persistent<true, 3, false, false, 768>, 768, 0, d, st); break;
+            case 16: rc = launch_persistent(render_persistent<true, 3, false, false, 768>, 768, 0, d, st); break;
+            case 17: rc = fits ? launch_persistent(render_persistent<true, 2, false, true, 512>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<true, 2, false, false, 512>, 512, 0, d, st); break;
             case 14: rc = fits ? launch_persistent(render_persistent<false, 4, false, true, 512>, 512, lds, d, st)
                                : launch_persistent(render_persistent<false, 4, false, false, 512>, 512, 0, d, st); break;
             case 19: rc = fits ? launch_persistent(render_persistent<true, 4, true, true, 512>, 512, lds, d, st)

@@ -1,0 +1,209 @@
+"""GPU tests of the rt.h boundary beyond the per-scene parity cases.
+
+All through the C ABI on cuda:0, each compared bit for bit (NaN positions
+equal) against the committed golden fixtures or the CPU oracle:
+golden vectors, stripe partitions (one process per rank, several contexts on
+one GPU), ragged/tiny sizes, max_depth edge values, >256 frames per call,
+image write/read and resume, caller-bound device image + caller stream, every
+kernel variant, the multi-device host gather, the RaytraceExecutor mirror, and
+the ABI's error behaviour.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import rtamd
+from helpers import bit_equal, gpu_image, mismatch_report, oracle_image
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _golden_cases():
+    with open(os.path.join(GOLDEN, "index.json")) as f:
+        return sorted(json.load(f).items(), key=lambda kv: int(kv[0]))
+
+
+@pytest.mark.parametrize("sid,case", _golden_cases(), ids=lambda v: v if isinstance(v, str) else "")
+def test_golden_fixtures(gpu, sid, case):
+    """Device render == the committed oracle fixture (no oracle call at run time)."""
+    s = rtamd.Scene(int(sid), case["width"], case["height"], seed=case["seed"])
+    g = np.load(os.path.join(GOLDEN, case["file"]))
+    out = gpu_image(s, case["frames"], max_depth=case["depth"], spp=case["spp"], seed=case["seed"])
+    assert bit_equal(out, g["image"]), mismatch_report(out, g["image"])
+
+
+@pytest.mark.parametrize("world,stripe", [(2, 16), (3, 4), (8, 1), (5, 64)])
+def test_stripe_partition_contexts(gpu, world, stripe):
+    """rt_set_partition: each rank's context renders only its stripes, stripe-compacted;
+    de-interleaved they equal the unpartitioned render."""
+    H, W = 45, 33
+    s = rtamd.Scene(8, W, H, seed=1)
+    full = gpu_image(s, 4)
+    padded = rtamd.padded_local_rows(H, world, stripe)
+    blocks = np.zeros((world, padded, W, 4), np.float32)
+    for r in range(world):
+        ctx = rtamd.RenderContext(devices=(0,), rank=r, world=world, stripe_rows=stripe)
+        ctx.upload_scene(s)
+        ctx.set_params(max_depth=5, spp=4)
+        ctx.resize(W, H)
+        ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+        loc = ctx.read_image()
+        assert loc.shape[0] == rtamd.local_rows(H, r, world, stripe)
+        blocks[r, :loc.shape[0]] = loc
+        ctx.close()
+    img = rtamd.deinterleave(blocks, H, world, stripe)
+    assert bit_equal(img, full), mismatch_report(img, full)
+
+
+def test_multi_device_context_host_gather(gpu):
+    """A context over several device slots (here device 0 twice) splits rows in stripes
+    and gathers on the host; equals the single-slot render."""
+    s = rtamd.Scene(6, 40, 37, seed=1)
+    a = gpu_image(s, 4)
+    b = gpu_image(s, 4, devices=(0, 0))
+    assert bit_equal(a, b), mismatch_report(a, b)
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (7, 3), (65, 9), (3, 70), (129, 1)])
+def test_ragged_sizes(gpu, w, h):
+    """Sizes that are not multiples of the 8x8 wave tile."""
+    s = rtamd.Scene(8, w, h, seed=1)
+    ref = oracle_image(s, 3)
+    out = gpu_image(s, 3)
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2, 50])
+def test_max_depth_edges(gpu, depth):
+    s = rtamd.Scene(7, 24, 24, seed=1)
+    ref = oracle_image(s, 3, max_depth=depth)
+    out = gpu_image(s, 3, max_depth=depth)
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
+def test_more_frames_than_one_launch(gpu):
+    """300 frames in one rt_render call (> RT_MAX_FRAMES_PER_LAUNCH = 256)."""
+    s = rtamd.Scene(3, 8, 8, seed=1)
+    ref = oracle_image(s, 300, spp=300)
+    out = gpu_image(s, 300, spp=300)
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
+def test_write_image_and_resume(gpu):
+    """rt_write_image + continue == uninterrupted progressive render (resume from a checkpoint)."""
+    s = rtamd.Scene(4, 20, 16, seed=1)
+    full = gpu_image(s, 6, spp=6)
+    ctx = rtamd.RenderContext()
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=6)
+    ctx.resize(20, 16)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 3))
+    half = ctx.read_image()
+    ctx.close()
+    ctx = rtamd.RenderContext()
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=6)
+    ctx.resize(20, 16)
+    ctx.write_image(half)
+    assert bit_equal(ctx.read_image(), half)
+    ctx.render(4, rtamd.frame_rand_factors(1, 3, 3))
+    out = ctx.read_image()
+    ctx.close()
+    assert bit_equal(out, full), mismatch_report(out, full)
+
+
+def test_bound_torch_image_and_stream(gpu):
+    """rt_bind_device_image + rt_set_stream: the kernel accumulates into a torch tensor on
+    torch's stream (the path bench.py times)."""
+    import torch
+    s = rtamd.Scene(8, 48, 27, seed=1)
+    ref = oracle_image(s, 4)
+    img = torch.zeros((27, 48, 4), dtype=torch.float32, device="cuda:0")
+    stream = torch.cuda.Stream(device=0)
+    ctx = rtamd.RenderContext()
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=4)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.bind_device_image(img.data_ptr(), img.numel() * 4)
+    ctx.resize(48, 27)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+    stream.synchronize()
+    out = img.cpu().numpy()
+    ctx.close()
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
+VARIANTS = [1, 2, 3, 4, 5, 10, 11, 12, 14, 20, 21, 22, 23]
+
+
+def test_all_kernel_variants_identical(gpu, monkeypatch):
+    """Every launch shape of the kernel (RT_KERNEL_VARIANT, used for A/B timing) renders the same bits."""
+    s = rtamd.Scene(8, 40, 24, seed=1)
+    ref = oracle_image(s, 4)
+    for v in VARIANTS:
+        monkeypatch.setenv("RT_KERNEL_VARIANT", str(v))
+        out = gpu_image(s, 4)
+        assert bit_equal(out, ref), f"variant {v}: {mismatch_report(out, ref)}"
+
+
+def test_stats_build_renders_same_bits(gpu):
+    """The diagnostic build (rt_debug_enable_stats) changes timing only."""
+    s = rtamd.Scene(8, 40, 24, seed=1)
+    ref = oracle_image(s, 2)
+    L = rtamd.amd()
+    ctx = rtamd.RenderContext()
+    assert L.rt_debug_enable_stats(ctx._h, 1) == 0
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=2)
+    ctx.resize(40, 24)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 2))
+    out = ctx.read_image()
+    stats = (ctypes.c_ulonglong * 64)()
+    assert L.rt_debug_read_stats(ctx._h, stats, 64) == 0
+    ctx.close()
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+    assert any(stats[k] for k in range(64))
+
+
+def test_executor_mirror(gpu):
+    """RaytraceExecutor: setSamplePerPixel, raytrace until sampleComplete, listeners fire once."""
+    s = rtamd.Scene(6, 16, 16, seed=9)
+    ctx = rtamd.RenderContext()
+    ctx.upload_scene(s)
+    ctx.resize(16, 16)
+    ex = rtamd.RaytraceExecutor(ctx, seed=9)
+    fired = []
+    ex.addCompleteListener(lambda: fired.append(ex.getNumSamples()))
+    ex.setSamplePerPixel(10)
+    while not ex.sampleComplete():
+        ex.raytrace(4)
+    assert ex.getNumSamples() == 10 and fired == [10] and ex.getFinishTime() >= 0
+    out = ctx.read_image()
+    ctx.close()
+    ref = oracle_image(s, 10, spp=10, seed=9)
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
+def test_error_behaviour(gpu):
+    L = rtamd.amd()
+    ctx = rtamd.RenderContext()
+    h = ctx._h
+    rf = rtamd.frame_rand_factors(1, 0, 1)
+    fp = rf.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    assert L.rt_render(h, 1, 1, fp) == -3                    # RT_ERR_STATE: nothing uploaded / no image
+    assert b"rt_resize" in L.rt_last_error(h) or b"BVH" in L.rt_last_error(h)
+    assert L.rt_upload_buffer(h, 0, b"\0" * 47, 47) == -1    # not a multiple of the 48-byte sphere record
+    assert L.rt_upload_buffer(h, 6, b"", 0) == -1            # no binding 6
+    assert L.rt_upload_texture(h, 8, 1, 1, 1, b"\0\0\0") == -4    # RT_ERR_LIMIT: slots 0..7
+    s = rtamd.Scene(6, 8, 8, seed=1)
+    ctx.upload_scene(s)
+    ctx.resize(8, 8)
+    assert L.rt_render(h, 0, 1, fp) == -1                    # frames are 1-based (frame_count = ++numSamples)
+    assert L.rt_render(h, 1, 1, None) == -1
+    with pytest.raises(rtamd.RTError, match="bad image size"):
+        ctx.resize(-1, 8)
+    ctx.close()

@@ -25,7 +25,7 @@ for s in $STEPS; do
     stats) run kstats 300 python tools/kernel_stats.py ${STATS_ARGS:-} ;;
     list)  run pmc_list 120 rocprofv3 -L ;;
     pmc)   run pmc 900 python tools/pmc_profile.py ${PMC_ARGS:-} ;;
-    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py ${BENCH_ARGS:-} ;;
   esac
 done
 exit 0

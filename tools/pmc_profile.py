@@ -40,11 +40,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "pmc.json"))
     ap.add_argument("--target", default="--scene 8 --frames 64")
+    ap.add_argument("--traffic-key", default="scene8_1920x1080_f64_d5")
+    ap.add_argument("--traffic-out", default=os.path.join(REPO, "gpurun_out", "traffic.json"))
+    ap.add_argument("--groups", default=None, help="comma list of group indices (default all)")
     a = ap.parse_args()
     listing = available() or ""
     res = {}
     os.makedirs(os.path.join(REPO, "gpurun_out", "pmc"), exist_ok=True)
+    sel = None if a.groups is None else {int(g) for g in a.groups.split(",")}
     for gi, grp in enumerate(GROUPS):
+        if sel is not None and gi not in sel:
+            continue
         grp = [c for c in grp if not listing or c in listing]
         if not grp:
             continue
@@ -68,17 +74,35 @@ def main():
                     val = float(row.get("Counter_Value", 0))
                     res.setdefault(name, 0.0)
                     res[name] += val
+    # per launch (render_once --launches 1 => one render dispatch per pass)
     if "FETCH_SIZE" in res:
         res["hbm_read_bytes_raw"] = res["FETCH_SIZE"] * 1024
         res["hbm_read_bytes_x2"] = res["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in res:
         res["hbm_write_bytes"] = res["WRITE_SIZE"] * 1024
+    if "hbm_read_bytes_x2" in res and "hbm_write_bytes" in res:
+        res["hbm_bytes_per_launch"] = res["hbm_read_bytes_x2"] + res["hbm_write_bytes"]
     if "SQ_THREAD_CYCLES_VALU" in res and "SQ_ACTIVE_INST_VALU" in res and res["SQ_ACTIVE_INST_VALU"]:
         res["valu_lane_utilization"] = res["SQ_THREAD_CYCLES_VALU"] / (64.0 * res["SQ_ACTIVE_INST_VALU"])
+    if "TCC_HIT_sum" in res and "TCC_MISS_sum" in res:
+        res["tcc_hit_rate"] = res["TCC_HIT_sum"] / max(1.0, res["TCC_HIT_sum"] + res["TCC_MISS_sum"])
     res["target"] = a.target
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
+    if a.traffic_key and "hbm_bytes_per_launch" in res:
+        # the entry bench.py reads as roofline.traffic
+        tj = {}
+        if os.path.exists(a.traffic_out):
+            with open(a.traffic_out) as f:
+                tj = json.load(f)
+        tj[a.traffic_key] = {k: res[k] for k in ("hbm_bytes_per_launch", "hbm_read_bytes_raw", "hbm_read_bytes_x2",
+                                                 "hbm_write_bytes") if k in res}
+        tj[a.traffic_key]["method"] = ("rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE in separate passes "
+                                       "(KB); reads x2 per the gfx950 FETCH_SIZE correction; one launch")
+        tj[a.traffic_key]["target"] = a.target
+        with open(a.traffic_out, "w") as f:
+            json.dump(tj, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
