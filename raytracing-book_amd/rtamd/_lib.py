@@ -57,6 +57,15 @@ def amd():
     """The product library (HIP).  Raises ImportError when it was not built."""
     global _amd
     if _amd is None:
+        # One HIP runtime per process.  torch ships its own libamdhip64 (SONAME
+        # libamdhip64.so.7, the name librtamd.so needs): loaded first, it is the
+        # one librtamd binds to, so torch tensors/streams handed to rt_bind_device_image
+        # / rt_set_stream belong to the same runtime.  Loaded after /opt/rocm's copy,
+        # torch would bring a second runtime that sees no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = _load("librtamd.so")
         vp, sz, i, f, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_float, ctypes.c_uint64
         _proto(L, "rt_abi_version", i)
