@@ -663,6 +663,7 @@ bool trace_through_bvh(Inv& I, const Ray& ray, Interval ray_t, HitRecord& rec) {
         if (hit_aabb(ray, ray_t, node)) {
             int node_type = node.left_id & 0xFFFF;
             if (node_type != 0) {
+                if (g_tlog) g_tlog->cur.back() |= 0x40000000;   // log: leaf reached, its prims tested
                 int model_idx = (node.left_id >> 16) & 0xFFFF;
                 for (int i = 0; i < 2; i++) {
                     if (hit_model(I, ray, ray_t, model_idx, node_type, rec)) {

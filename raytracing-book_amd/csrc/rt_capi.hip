@@ -197,6 +197,12 @@ int thread_bvh(rt_ctx* c, const rt_bvh_node* in, int n, std::vector<rt_dnode>& o
         uint32_t lt = (uint32_t)(nd.left_id & 0xFFFF), rt = (uint32_t)(nd.right_id & 0xFFFF);
         if (lt != 0) {
             if (lt > 15 || rt > 15 || rt == 0) return set_err(c, RT_ERR_INVALID_ARG, "BVH leaf with bad model type");
+            // A singleton leaf lists one prim twice (BVHNode.java:33-34).
+            // Re-testing a sphere cannot hit (strict root test against the t it set);
+            // a quad/box re-hit at equal t rebuilds the same record (same face: the
+            // last interior face of minimal t).  Only a medium's second test matters
+            // (its own rand() draw), so for the others slot 2 is marked empty (type 0).
+            if (lt == rt && nd.left_id == nd.right_id && lt != RT_MODEL_CONSTANT_MEDIUM) rt = 0;
             d.meta = skip | (lt << 16) | (rt << 20);
             d.prims = (uint32_t)((nd.left_id >> 16) & 0xFFFF) | ((uint32_t)((nd.right_id >> 16) & 0xFFFF) << 16);
         } else {
@@ -467,7 +473,7 @@ int rt_bind_device_image(rt_ctx* c, void* ptr, size_t nbytes) {
         d.image_bound = false;
         return RT_OK;
     }
-    if (nbytes < (size_t)d.padded_rows * c->width * 16) return set_err(c, RT_ERR_INVALID_ARG, "device image too small");
+    if (nbytes < (size_t)d.local_rows * c->width * 16) return set_err(c, RT_ERR_INVALID_ARG, "device image too small");
     d.image_ptr = (float*)ptr;
     d.image_bound = true;
     return RT_OK;
@@ -709,7 +715,13 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
         if (d.stats.ptr) HIPCHK(c, hipMemsetAsync(d.stats.ptr, 0, d.stats.bytes, d.stream));
         HIPCHK(c, hipStreamSynchronize(d.stream));
     }
-    c->variant = on ? ((c->variant >= 20) ? 29 : ((c->variant == 0 || c->variant >= 10) ? 19 : 9)) : 0;
+    // stats twin of the current launch shape: 0/30 -> 31, 10..19 -> 19, 20..29 -> 29, grid -> 9
+    if (on) {
+        int v = c->variant;
+        c->variant = (v == 0 || v >= 30) ? 31 : (v >= 20) ? 29 : (v >= 10) ? 19 : 9;
+    } else {
+        c->variant = 0;
+    }
     return RT_OK;
 }
 

@@ -248,6 +248,47 @@ __device__ __forceinline__ void slab(float mn, float mx, float o, float inv, flo
     hi = (b < hi) ? b : hi;
 }
 
+// hit_aabb (hitting.glsl:55-76) with NaN-ignoring min/max: the reference's
+// per-axis swap + conditional updates are lo = max({tmin} U near_i), hi =
+// min({tmax} U far_i) over the non-NaN candidates, and v_min/v_max (IEEE
+// minNum/maxNum) ignore a NaN operand.  A slab value is NaN only when
+// inv = +-inf (dir component +-0 or denormal-small) and the origin lies on the
+// slab plane; with inv = +inf the reference's asymmetric NaN handling still
+// equals min/max, with inv = -inf it does not, so rays with an inv component
+// of -inf take the exact path (slab()).  Signed zeros differ only where
+// hi <= lo holds either way (lo >= tmin = 0.001 > 0).
+// The instructions themselves: the compiler wraps fminf/fmaxf operands in
+// canonicalizing moves (sNaN quieting), which our operands never need (their
+// only NaNs are quiet 0*inf products).
+__device__ __forceinline__ float v_min(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float v_max(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float v_min3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float v_max3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ bool aabb_fast(float4 n0, float4 n1, v3 o, v3 inv, float tmin, float tmax) {
+    float t0x = (n0.x - o.x) * inv.x, t1x = (n0.y - o.x) * inv.x;
+    float t0y = (n0.z - o.y) * inv.y, t1y = (n0.w - o.y) * inv.y;
+    float t0z = (n1.x - o.z) * inv.z, t1z = (n1.y - o.z) * inv.z;
+    float lo = v_max(v_max3(tmin, v_min(t0x, t1x), v_min(t0y, t1y)), v_min(t0z, t1z));
+    float hi = v_min(v_min3(tmax, v_max(t0x, t1x), v_max(t0y, t1y)), v_max(t0z, t1z));
+    return !(hi <= lo);
+}
+
 // The two prims of a leaf (compute.glsl:247-256), left then right.
 template <bool STATS>
 __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a, float time,
@@ -291,7 +332,7 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
 //   WHILE_WHILE: lanes advance through inner/missed nodes until each holds a
 //                hit leaf (or is done), then the leaves are tested together;
 //   else       : one node per iteration, leaf tests inline (if-if).
-template <bool WHILE_WHILE, bool STATS>
+template <int WHILE_WHILE, bool STATS>
 __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ nodes, v3 o, v3 d, float time,
                                       float& rf, float px, float py, Hit& h, unsigned long long* st) {
     if (P.n_nodes == 0) return false;
@@ -300,7 +341,47 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
     float a = g_dot(d, d);
     bool has = false;
     uint32_t i = 0;
-    if (WHILE_WHILE) {
+    // rays that need the exact slab (see aabb_fast); wave-uniform fast path otherwise
+    const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
+    const bool wave_exact = (WHILE_WHILE & 2) ? (__ballot(lane_exact) != 0) : true;   // uniform
+    if (WHILE_WHILE & 2) {
+        // while-while with a branch-free node step and one loop exit: a hit inner
+        // node continues at i+1 (its right child), anything else at the skip
+        // link; a hit leaf leaves the loop with its prims pending.
+        for (;;) {
+            uint32_t meta = 0, prims = 0;
+            bool leaf = false;
+            unsigned long long t0 = STATS ? clock64() : 0;
+            if (i != RT_NODE_END) {
+                for (;;) {
+                    if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
+                    float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
+                    meta = __float_as_uint(n1.z);
+                    prims = __float_as_uint(n1.w);
+                    bool hitn;
+                    if (!wave_exact) {
+                        hitn = aabb_fast(n0, n1, o, inv, tmin, tmax);
+                    } else {
+                        float lo = tmin, hi = tmax;
+                        slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+                        slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+                        slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+                        hitn = !(hi <= lo);
+                    }
+                    bool inner = (meta & 0xF0000u) == 0;
+                    i = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
+                    leaf = hitn && !inner;
+                    if (leaf || i == RT_NODE_END) break;
+                }
+            }
+            if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
+            if (!leaf) break;
+            unsigned long long t1 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+            leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+        }
+    } else if (WHILE_WHILE & 1) {
         for (;;) {
             uint32_t meta = 0, prims = 0;
             bool leaf = false;
@@ -760,7 +841,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 }
 
 // One iteration of ray_color's loop (compute.glsl:304-340).
-template <bool WW, bool STATS>
+template <int WW, bool STATS>
 __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, Path& S, float px, float py,
                                        v3& result, unsigned long long* st) {
     if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
@@ -836,7 +917,7 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
 // column x of local (stripe-compacted) row lr.  Path regeneration: a lane whose
 // path ended starts its next frame at once; each pixel still runs its frames
 // in order and applies the running mean per frame.
-template <bool WW, bool STATS>
+template <int WW, bool STATS>
 __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, int x, int lr,
                                              unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
@@ -945,7 +1026,7 @@ __device__ __forceinline__ void render_pixel_uniform(const KP& P, const float4* 
 }
 
 // Grid-per-image variant (A/B reference): 16x16 workgroups, one pixel each.
-template <bool WW, int MINW, bool STATS>
+template <int WW, int MINW, bool STATS>
 __global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     __shared__ unsigned long long s_stats[STATS ? 4 : 1][STATS ? ST_N : 1];
@@ -979,7 +1060,7 @@ __global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict_
 // repeatedly takes the next 8x8 pixel tile from a device-wide counter (one
 // returning atomic per tile) until the counter passes the last tile — a
 // condition every wave reaches.
-template <bool WW, int MINW, bool STATS, bool LDSN, int BLOCK, bool UNI = false>
+template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, bool UNI = false>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
@@ -1070,7 +1151,8 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
     const rt_kernel_args* d = (const rt_kernel_args*)dargs;
     // Variants (A/B only; all bit-identical):
-    //   persistent (default 0 = 10): 10 WW/512/4w, 11 WW/640/5w, 12 WW/512/4w global nodes,
+    //   persistent (default 0 = 30): 30 WW + fast slab + branch-free node step /512/4w, 31 stats of 30,
+    //                                10 WW/512/4w, 11 WW/640/5w, 12 WW/512/4w global nodes,
     //                                14 if-if/512/4w, 15 WW/768/3w, 16 WW/768/3w global nodes,
     //                                17 WW/512/2w, 19 stats of 10
     //   grid per image: 1 if-if, 2 WW 4w, 3 WW 5w, 4 if-if 4w, 5 WW default, 9 stats of 5
@@ -1083,6 +1165,10 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
             case 11: rc = fits ? launch_persistent(render_persistent<true, 5, false, true, 640>, 640, lds, d, st)
                                : launch_persistent(render_persistent<true, 5, false, false, 640>, 640, 0, d, st); break;
             case 12: rc = launch_persistent(render_persistent<true, 4, false, false, 512>, 512, 0, d, st); break;
+            case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
+            case 31: rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<3, 4, true, false, 512>, 512, 0, d, st); break;
             case 15: rc = fits ? launch_persistent(render_persistent<true, 3, false, true, 768>, 768, lds, d, st)
                                : launch_persistent(render_persistent<true, 3, false, false, 768>, 768, 0, d, st); break;
             case 16: rc = launch_persistent(render_persistent<true, 3, false, false, 768>, 768, 0, d, st); break;
@@ -1101,8 +1187,10 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
                                : launch_persistent(render_persistent<true, 4, false, false, 1024, true>, 1024, 0, d, st); break;
             case 29: rc = fits ? launch_persistent(render_persistent<true, 4, true, true, 512, true>, 512, lds, d, st)
                                : launch_persistent(render_persistent<true, 4, true, false, 512, true>, 512, 0, d, st); break;
-            default: rc = fits ? launch_persistent(render_persistent<true, 4, false, true, 512>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<true, 4, false, false, 512>, 512, 0, d, st); break;
+            case 10: rc = fits ? launch_persistent(render_persistent<1, 4, false, true, 512>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<1, 4, false, false, 512>, 512, 0, d, st); break;
+            default: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
+                               : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
         }
         if (rc) return rc;
         return hipGetLastError() == hipSuccess ? 0 : -1;

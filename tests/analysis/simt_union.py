@@ -46,6 +46,7 @@ def main():
             groups.setdefault((fr, b), []).append(buf[k + 4:k + 4 + m])
             k += 4 + m
         for (fr, b), seqs in groups.items():
+            seqs = [x & 0x3FFFFFFF for x in seqs]
             u = len(set(np.concatenate(seqs).tolist()))
             s = sum(len(x) for x in seqs)
             mx = max(len(x) for x in seqs)

@@ -140,7 +140,10 @@ def stack_visits(nodes_bytes, seed, p):
         k = stack.pop()
         hit = _pred(box[k], seed, p)
         lt = ids[k, 0] & 0xFFFF
-        leaf = (lt, (ids[k, 0] >> 16) & 0xFFFF, ids[k, 1] & 0xFFFF, (ids[k, 1] >> 16) & 0xFFFF) if lt else None
+        rt = ids[k, 1] & 0xFFFF
+        if lt and ids[k, 0] == ids[k, 1] and lt != 3:
+            rt = 0   # re-layout drops the redundant second test of a non-medium singleton leaf
+        leaf = (lt, (ids[k, 0] >> 16) & 0xFFFF, rt, (ids[k, 1] >> 16) & 0xFFFF) if lt else None
         seq.append((box[k].tobytes(), hit, leaf if hit else None))
         if hit and not lt:
             stack += [(ids[k, 0] >> 16) & 0xFFFF, (ids[k, 1] >> 16) & 0xFFFF]

@@ -128,8 +128,8 @@ def test_bound_torch_image_and_stream(gpu):
     ctx.upload_scene(s)
     ctx.set_params(max_depth=5, spp=4)
     ctx.set_stream(stream.cuda_stream)
+    ctx.resize(48, 27)                                    # sizes the image the bound buffer must hold
     ctx.bind_device_image(img.data_ptr(), img.numel() * 4)
-    ctx.resize(48, 27)
     ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
     stream.synchronize()
     out = img.cpu().numpy()
@@ -137,7 +137,7 @@ def test_bound_torch_image_and_stream(gpu):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
-VARIANTS = [1, 2, 3, 4, 5, 10, 11, 12, 14, 20, 21, 22, 23]
+VARIANTS = [1, 2, 3, 4, 5, 10, 11, 12, 14, 15, 16, 17, 20, 21, 22, 23, 30]
 
 
 def test_all_kernel_variants_identical(gpu, monkeypatch):
