@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--frames-per-step", type=int, default=64, help="spp per step per rank")
     p.add_argument("--depth", type=int, default=5)
     p.add_argument("--spp-total", type=int, default=4096, help="sqrt_spp uniform (BASELINE C3: 4096)")
-    p.add_argument("--stripe-rows", type=int, default=16)
+    p.add_argument("--stripe-rows", type=int, default=8)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")

@@ -37,7 +37,8 @@ struct Device {
     DevBuf image;            // internal image
     DevBuf args;             // rt_kernel_args slot in device memory
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
-    DevBuf counter;          // persistent-kernel tile counter
+    DevBuf counter;          // persistent-kernel work-unit counter
+    DevBuf samples;          // chunked launches: per-frame colours
     static constexpr int kRing = 8;
     rt_kernel_args* ring = nullptr;   // pinned host staging slots for async arg uploads
     hipEvent_t ring_ev[kRing] = {};
@@ -69,6 +70,11 @@ struct rt_ctx {
     bool validated = false;
     uint64_t last_ns = 0;
     int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
+    // Work split: aim for chunk_target work units per resident wave (env
+    // RT_CHUNK_TARGET; 0 = one chunk = direct mode).  Chunked launches stage
+    // per-frame colours in a device buffer of at most sample_budget bytes.
+    int chunk_target = 32;
+    size_t sample_budget = (size_t)4 << 30;
 };
 
 namespace {
@@ -300,6 +306,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
         return fail(RT_ERR_INVALID_ARG, "rt_create: bad device count");
     rt_ctx* c = new rt_ctx();
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) c->variant = std::atoi(v);
+    if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
         Device& d = c->devs[i];
@@ -324,7 +331,7 @@ int rt_destroy(rt_ctx* c) {
         (void)hipSetDevice(d.id);
         (void)hipStreamSynchronize(d.stream);
         dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
-        dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter);
+        dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter); dev_free(d.samples);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
             if (e) (void)hipEventDestroy(e);
@@ -552,11 +559,37 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             for (auto& e : d.ring_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         a.tile_counter = (int*)d.counter.ptr;
+        a.n_pixels = (size_t)d.local_rows * c->width;
+        // Frames per launch and the unit split.  Units = tiles x chunks; with too
+        // few tiles per resident wave (small images, N-GPU stripes) the frames
+        // are chunked so the dynamic schedule has enough units to balance.
+        const int n_tiles = ((c->width + 7) / 8) * ((d.local_rows + 7) / 8);
+        int per_launch = RT_MAX_FRAMES_PER_LAUNCH;
+        int chunks_wanted = 1;
+        if (c->chunk_target > 0 && n_tiles > 0) {
+            long long waves = rt_resident_waves();
+            chunks_wanted = (int)std::min<long long>(RT_MAX_FRAMES_PER_LAUNCH,
+                                                     (c->chunk_target * waves + n_tiles - 1) / n_tiles);
+        }
+        if (chunks_wanted > 1) {
+            size_t per_frame = a.n_pixels * sizeof(float4);
+            per_launch = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, c->sample_budget / per_frame));
+            size_t need = per_frame * (size_t)std::min(per_launch, n_frames);
+            if (d.samples.bytes < need) {
+                dev_free(d.samples);
+                HIPCHK(c, hipMalloc(&d.samples.ptr, need));
+                d.samples.bytes = need;
+            }
+        }
         HIPCHK(c, hipEventRecord(d.ev_start, d.stream));
-        for (int f0 = 0; f0 < n_frames; f0 += RT_MAX_FRAMES_PER_LAUNCH) {
-            int nf = std::min(RT_MAX_FRAMES_PER_LAUNCH, n_frames - f0);
+        for (int f0 = 0; f0 < n_frames; f0 += per_launch) {
+            int nf = std::min(per_launch, n_frames - f0);
             a.first_frame = first_frame + f0;
             a.n_frames = nf;
+            a.n_chunks = std::max(1, std::min(chunks_wanted, nf));
+            a.chunk_frames = (nf + a.n_chunks - 1) / a.n_chunks;
+            a.n_chunks = (nf + a.chunk_frames - 1) / a.chunk_frames;
+            a.samples = a.n_chunks > 1 ? (float4*)d.samples.ptr : nullptr;
             std::memcpy(a.rand_factors, rand_factors + f0, sizeof(float) * nf);
             int slot = d.ring_pos++ % Device::kRing;
             HIPCHK(c, hipEventSynchronize(d.ring_ev[slot]));   // the copy that last used this slot is done
@@ -715,10 +748,10 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
         if (d.stats.ptr) HIPCHK(c, hipMemsetAsync(d.stats.ptr, 0, d.stats.bytes, d.stream));
         HIPCHK(c, hipStreamSynchronize(d.stream));
     }
-    // stats twin of the current launch shape: 0/30 -> 31, 10..19 -> 19, 20..29 -> 29, grid -> 9
+    // stats twin of the current launch shape: 0/12/15/30 -> 31, 10 -> 19
     if (on) {
         int v = c->variant;
-        c->variant = (v == 0 || v >= 30) ? 31 : (v >= 20) ? 29 : (v >= 10) ? 19 : 9;
+        c->variant = (v == 10 || v == 19) ? 19 : 31;
     } else {
         c->variant = 0;
     }

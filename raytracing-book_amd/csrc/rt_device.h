@@ -10,8 +10,10 @@
 //   lights   : int32 packed ids
 //   textures : RGB8 expanded to RGBA8 (4 B/texel, aligned), RGBA8, R32F
 //   image    : float4 [padded_local_rows][W], stripe-compacted rows
+//   samples  : float4 [frames][local_rows*W] per-frame colours (chunked launches only)
 #pragma once
 
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "rt/rt_types.h"
@@ -62,11 +64,16 @@ struct rt_kernel_args {
     int rank, world, stripe_rows;
     int first_frame, n_frames;
     unsigned long long* stats;   // diagnostic counters (stats variant only)
-    int* tile_counter;           // persistent variants: next 8x8 tile (zeroed per launch)
+    int* tile_counter;           // persistent kernel: next work unit (zeroed per launch)
+    // work split: unit = chunk * n_tiles + tile, chunk = frames [c*chunk_frames, ...)
+    int n_chunks, chunk_frames;
+    float4* samples;             // chunked mode: per-frame colours [n_frames][n_pixels]; nullptr = direct
+    size_t n_pixels;             // local_rows * width
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
 };
 
 // launcher implemented in rt_kernel.hip
+int rt_resident_waves(void);   // waves the default launch shape keeps resident on the current device
 int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream);
 // debug: evaluate GLSL built-ins on device (tests)
 int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream);

@@ -328,10 +328,10 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
 }
 
 // compute.glsl:226-266 over the threaded BVH.  Each lane's node sequence is the
-// reference's; only the interleaving of a wave's lanes differs:
-//   WHILE_WHILE: lanes advance through inner/missed nodes until each holds a
-//                hit leaf (or is done), then the leaves are tested together;
-//   else       : one node per iteration, leaf tests inline (if-if).
+// reference's; only the interleaving of a wave's lanes differs: lanes advance
+// through inner/missed nodes until each holds a hit leaf (or is done), then the
+// leaves are tested together ("while-while").  WHILE_WHILE bit 1 selects the
+// branch-free node step with the NaN-exact min/max slab test.
 template <int WHILE_WHILE, bool STATS>
 __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ nodes, v3 o, v3 d, float time,
                                       float& rf, float px, float py, Hit& h, unsigned long long* st) {
@@ -381,7 +381,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
             leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
             if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
         }
-    } else if (WHILE_WHILE & 1) {
+    } else {
         for (;;) {
             uint32_t meta = 0, prims = 0;
             bool leaf = false;
@@ -408,80 +408,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
             if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
             i = meta & 0xFFFFu;
         }
-    } else {
-        while (i != RT_NODE_END) {
-            float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
-            uint32_t meta = __float_as_uint(n1.z);
-            uint32_t prims = __float_as_uint(n1.w);
-            float lo = tmin, hi = tmax;
-            slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-            slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-            slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-            uint32_t skip = meta & 0xFFFFu;
-            if (hi <= lo) { i = skip; continue; }
-            if (((meta >> 16) & 0xFu) == 0) { i = i + 1; continue; }
-            leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
-            i = skip;
-        }
     }
-    return has;
-}
-
-// Minimum over the 64 lanes (DPP row shifts + row broadcasts); EXEC must be full.
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    const int ID = (int)0xFFFFFFFFu;
-    uint32_t x = v, y;
-    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x111, 0xf, 0xf, false); x = y < x ? y : x;   // row_shr:1
-    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x112, 0xf, 0xf, false); x = y < x ? y : x;   // row_shr:2
-    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x114, 0xf, 0xf, false); x = y < x ? y : x;   // row_shr:4
-    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x118, 0xf, 0xf, false); x = y < x ? y : x;   // row_shr:8
-    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x142, 0xa, 0xf, false); x = y < x ? y : x;   // row_bcast:15
-    y = (uint32_t)__builtin_amdgcn_update_dpp(ID, (int)x, 0x143, 0xc, 0xf, false); x = y < x ? y : x;   // row_bcast:31
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-}
-
-// compute.glsl:226-266, wave-uniform schedule.  Every lane's visit sequence is
-// an increasing subsequence of the right-first pre-order array, so the wave
-// walks node i = min over lanes of next[lane]: lanes with next == i take their
-// reference step (AABB test; inner hit -> i+1, leaf hit -> its two prims, miss
-// or leaf done -> skip) and the others wait.  Each lane's node order, ray_t
-// updates and rand() draws are exactly its own reference sequence; the node
-// record is a broadcast read and a leaf's prim type/index are wave-uniform.
-// Called by all 64 lanes (EXEC full); lanes with want == false do not walk.
-template <bool STATS>
-__device__ __forceinline__ bool trace_uniform(const KP& P, const float4* __restrict__ nodes, bool want, v3 o, v3 d,
-                                              float time, float& rf, float px, float py, Hit& h,
-                                              unsigned long long* st) {
-    uint32_t n = (want && P.n_nodes > 0) ? 0u : RT_NODE_END;
-    float tmin = 0.001f, tmax = RT_INFINITY;
-    v3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    float a = g_dot(d, d);
-    bool has = false;
-    uint32_t i = wave_min_u32(n);
-    unsigned long long t0 = STATS ? clock64() : 0;
-    while (i != RT_NODE_END) {
-        float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
-        uint32_t meta = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(n1.z));
-        uint32_t prims = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(n1.w));
-        uint32_t skip = meta & 0xFFFFu;
-        bool is_leaf = ((meta >> 16) & 0xFu) != 0;
-        bool part = (n == i);
-        if (STATS) st_pred(st, part, ST_NODE_IT, ST_NODE_LN);
-        float lo = tmin, hi = tmax;
-        slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-        slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-        slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-        bool hitb = part && !(hi <= lo);
-        if (part) n = (hitb && !is_leaf) ? i + 1 : skip;
-        if (is_leaf && __ballot(hitb) != 0) {
-            unsigned long long t1 = STATS ? clock64() : 0;
-            if (STATS) st_pred(st, hitb, ST_LEAF_IT, ST_LEAF_LN);
-            if (hitb) leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
-            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-        }
-        i = (__ballot(n == i + 1) != 0) ? i + 1 : wave_min_u32(n);
-    }
-    if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
     return has;
 }
 
@@ -913,27 +840,33 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
     S.uvs.kind_idx = 0; S.uvs.a = 0.0f; S.uvs.b = 0.0f; S.uvs.c = 0.0f;
 }
 
-// compute.glsl:345-358 for all frames of the launch, for the pixel at
+// compute.glsl:345-358 for frames [f0, f1) of the launch, for the pixel at
 // column x of local (stripe-compacted) row lr.  Path regeneration: a lane whose
 // path ended starts its next frame at once; each pixel still runs its frames
-// in order and applies the running mean per frame.
+// in order.  Direct mode (P.samples == nullptr): the running mean is applied
+// per frame in registers and the image is read/written once.  Chunked mode:
+// each frame's colour goes to P.samples[f][pixel] and fold_kernel applies the
+// running mean afterwards in frame order (the same operations, so the same bits).
 template <int WW, bool STATS>
-__device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, int x, int lr,
-                                             unsigned long long* st) {
+__device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, int x, int lr, int f0,
+                                             int f1, unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
     int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
-    float4* px = reinterpret_cast<float4*>(P.image) + (size_t)lr * P.width + x;
-    float4 prev = *px;
+    const size_t pix = (size_t)lr * P.width + x;
+    float4* px = reinterpret_cast<float4*>(P.image) + pix;
+    const bool direct = P.samples == nullptr;
+    float4 prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (direct) prev = *px;
     const rt_camera_ubo& C = P.cam;
     float fx = (float)x, fy = (float)y;
     // get_norm_coord (compute.glsl:268-283) before its jitter term: per pixel
     v3 base = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
     Path S;
-    int f = 0;
+    int f = f0;
     bool fresh = true;
     for (;;) {
         if (fresh) {
-            if (f >= P.n_frames) break;
+            if (f >= f1) break;
             unsigned long long t0 = STATS ? clock64() : 0;
             if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
             start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, base);
@@ -942,125 +875,31 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
         }
         v3 cur;
         if (bounce<WW, STATS>(P, nodes, S, fx, fy, cur, st)) {
-            int fc = P.first_frame + f;
-            float n1 = (float)(fc - 1), n = (float)fc;
-            prev.x = (prev.x * n1 + cur.x) / n;
-            prev.y = (prev.y * n1 + cur.y) / n;
-            prev.z = (prev.z * n1 + cur.z) / n;
-            prev.w = 1.0f;
+            if (direct) {
+                int fc = P.first_frame + f;
+                float n1 = (float)(fc - 1), n = (float)fc;
+                prev.x = (prev.x * n1 + cur.x) / n;
+                prev.y = (prev.y * n1 + cur.y) / n;
+                prev.z = (prev.z * n1 + cur.z) / n;
+                prev.w = 1.0f;
+            } else {
+                P.samples[(size_t)f * P.n_pixels + pix] = make_float4(cur.x, cur.y, cur.z, 0.0f);
+            }
             f++;
             fresh = true;
         }
     }
-    *px = prev;
+    if (direct) *px = prev;
 }
 
-// ray_color for a whole wave with the wave-uniform walk: frames run in
-// lock-step per wave (no regeneration), so each bounce's walk is shared by the
-// lanes still alive.  Called by all 64 lanes; `valid` lanes own a pixel.
-template <bool STATS>
-__device__ __forceinline__ void render_pixel_uniform(const KP& P, const float4* __restrict__ nodes, int x, int lr,
-                                                     bool valid, unsigned long long* st) {
-    int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
-    int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
-    float4* px = reinterpret_cast<float4*>(P.image) + ((size_t)lr * P.width + x);
-    float4 prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (valid) prev = *px;
-    const rt_camera_ubo& C = P.cam;
-    float fx = (float)x, fy = (float)y;
-    v3 base = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
-    Path S;
-    S.o = mk3s(0.0f); S.d = mk3s(0.0f); S.acc = mk3s(0.0f); S.time = 0.0f; S.rf = 0.0f; S.depth = 0;
-    S.uvs.kind_idx = 0; S.uvs.a = 0.0f; S.uvs.b = 0.0f; S.uvs.c = 0.0f;
-    for (int f = 0; f < P.n_frames; f++) {
-        if (valid) {
-            unsigned long long t0 = STATS ? clock64() : 0;
-            if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
-            start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, base);
-            if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
-        }
-        bool alive = valid;
-        v3 cur = mk3s(0.0f);
-        while (__ballot(alive) != 0) {
-            // compute.glsl:304 loop bound; final_color stays vec3(0) when exhausted
-            if (alive && S.depth >= P.max_depth) { cur = mk3s(0.0f); alive = false; }
-            bool go = alive;
-            if (go) S.depth++;
-            v3 d = S.d;
-            // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
-            bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
-            Hit h;
-            h.t = 0.0f; h.type = 0; h.idx = 0; h.face = 0;
-            h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
-            bool hit = trace_uniform<STATS>(P, nodes, go && !dir_zero, S.o, d, S.time, S.rf, fx, fy, h, st);
-            if (go) {
-                unsigned long long ts = STATS ? clock64() : 0;
-                if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
-                if (h.uv_kind_idx != 0) {
-                    bool sph = (h.uv_kind_idx >> 16) == 1;
-                    v3 up = add3(S.o, scale3(d, h.uv_a));
-                    S.uvs.kind_idx = h.uv_kind_idx;
-                    S.uvs.a = sph ? up.x : h.uv_a;
-                    S.uvs.b = sph ? up.y : h.uv_b;
-                    S.uvs.c = sph ? up.z : S.uvs.c;
-                }
-                if (!hit) {
-                    cur = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
-                    alive = false;
-                } else if (shade(P, S, h, fx, fy, cur)) {
-                    alive = false;
-                }
-                if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
-            }
-        }
-        if (valid) {
-            int fc = P.first_frame + f;
-            float n1 = (float)(fc - 1), nn = (float)fc;
-            prev.x = (prev.x * n1 + cur.x) / nn;
-            prev.y = (prev.y * n1 + cur.y) / nn;
-            prev.z = (prev.z * n1 + cur.z) / nn;
-            prev.w = 1.0f;
-        }
-    }
-    if (valid) *px = prev;
-}
-
-// Grid-per-image variant (A/B reference): 16x16 workgroups, one pixel each.
-template <int WW, int MINW, bool STATS>
-__global__ void __launch_bounds__(256, MINW) render_kernel(const KP* __restrict__ Pp) {
-    const KP& P = *Pp;
-    __shared__ unsigned long long s_stats[STATS ? 4 : 1][STATS ? ST_N : 1];
-    unsigned long long* st = nullptr;
-    unsigned long long t_begin = 0;
-    int tid = threadIdx.y * 16 + threadIdx.x;
-    if (STATS) {
-        for (int k = tid; k < 4 * ST_N; k += 256) (&s_stats[0][0])[k] = 0;
-        __syncthreads();
-        st = s_stats[tid / 64];
-        t_begin = clock64();
-    }
-    int x = blockIdx.x * 16 + threadIdx.x;
-    int lr = blockIdx.y * 16 + threadIdx.y;
-    bool active = x < P.width && lr < P.local_rows;
-    if (!STATS && !active) return;
-    if (active) render_pixel<WW, STATS>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, st);
-    if (STATS) {
-        st_add(st, ST_TOTAL, clock64() - t_begin);
-        __syncthreads();
-        if (tid < ST_N) {
-            unsigned long long v = 0;
-            for (int w = 0; w < 4; w++) v += s_stats[w][tid];
-            atomicAdd(P.stats + tid, v);
-        }
-    }
-}
-
-// Persistent variant (default): one resident grid; each workgroup stages the
-// threaded BVH (32 B/node, 57 KB for scene 8) in LDS once, then each wave
-// repeatedly takes the next 8x8 pixel tile from a device-wide counter (one
-// returning atomic per tile) until the counter passes the last tile — a
-// condition every wave reaches.
-template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, bool UNI = false>
+// Persistent kernel: one resident grid; each workgroup stages the threaded BVH
+// (32 B/node, 57 KB for scene 8) in LDS once, then each wave repeatedly takes
+// the next work unit from a device-wide counter (one returning atomic per
+// unit) until the counter passes the last unit — a condition every wave
+// reaches.  A unit is one 8x8 pixel tile x one chunk of the launch's frames
+// (unit = chunk * n_tiles + tile), so a launch over few tiles (a narrow stripe
+// set at N GPUs) still has many more units than resident waves.
+template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
@@ -1081,22 +920,20 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
     if (STATS) t_begin = clock64();
     const int tiles_x = (P.width + 7) >> 3;
     const int n_tiles = tiles_x * ((P.local_rows + 7) >> 3);
+    const int n_units = n_tiles * P.n_chunks;
     for (;;) {
-        int tile = 0;
-        if (lane == 0) tile = atomicAdd(P.tile_counter, 1);
-        tile = __shfl(tile, 0);
-        if (tile >= n_tiles) break;
+        int unit = 0;
+        if (lane == 0) unit = atomicAdd(P.tile_counter, 1);
+        unit = __shfl(unit, 0);
+        if (unit >= n_units) break;
+        const int chunk = unit / n_tiles, tile = unit - chunk * n_tiles;
+        const int f0 = chunk * P.chunk_frames;
+        const int f1 = min(P.n_frames, f0 + P.chunk_frames);
         int x = (tile % tiles_x) * 8 + (lane & 7);
         int lr = (tile / tiles_x) * 8 + (lane >> 3);
-        bool valid = x < P.width && lr < P.local_rows;
-        if (UNI) {
-            // every lane enters (EXEC stays full for the wave-uniform walk)
-            int xc = valid ? x : 0, lc = valid ? lr : 0;
-            if (LDSN) render_pixel_uniform<STATS>(P, s_nodes, xc, lc, valid, st);
-            else render_pixel_uniform<STATS>(P, reinterpret_cast<const float4*>(P.nodes), xc, lc, valid, st);
-        } else if (valid) {
-            if (LDSN) render_pixel<WW, STATS>(P, s_nodes, x, lr, st);
-            else render_pixel<WW, STATS>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, st);
+        if (x < P.width && lr < P.local_rows) {
+            if (LDSN) render_pixel<WW, STATS>(P, s_nodes, x, lr, f0, f1, st);
+            else render_pixel<WW, STATS>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, f0, f1, st);
         }
     }
     if (STATS) {
@@ -1108,6 +945,27 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             atomicAdd(P.stats + tid, v);
         }
     }
+}
+
+// Chunked mode epilogue: the running mean of compute.glsl:355 over the
+// launch's frames, in frame order, per pixel: (prev*(n-1)+cur)/n.
+__global__ void __launch_bounds__(256) fold_kernel(const KP* __restrict__ Pp) {
+    const KP& P = *Pp;
+    const size_t pix = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (pix >= P.n_pixels) return;
+    float4* px = reinterpret_cast<float4*>(P.image) + pix;
+    float4 prev = *px;
+    const float4* s = P.samples + pix;
+    for (int f = 0; f < P.n_frames; f++) {
+        float4 cur = s[(size_t)f * P.n_pixels];
+        int fc = P.first_frame + f;
+        float n1 = (float)(fc - 1), n = (float)fc;
+        prev.x = (prev.x * n1 + cur.x) / n;
+        prev.y = (prev.y * n1 + cur.y) / n;
+        prev.z = (prev.z * n1 + cur.z) / n;
+        prev.w = 1.0f;
+    }
+    *px = prev;
 }
 
 __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const float* __restrict__ y,
@@ -1141,6 +999,13 @@ int launch_persistent(K kernel, int block, size_t lds, const rt_kernel_args* d, 
 
 }  // namespace
 
+int rt_resident_waves(void) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return cus * 2 * (512 / 64);   // default shape: 2 workgroups of 512 per CU
+}
+
 int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
     // Arguments live in device memory: the by-value kernarg struct would be copied
@@ -1151,59 +1016,30 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
     const rt_kernel_args* d = (const rt_kernel_args*)dargs;
     // Variants (A/B only; all bit-identical):
-    //   persistent (default 0 = 30): 30 WW + fast slab + branch-free node step /512/4w, 31 stats of 30,
-    //                                10 WW/512/4w, 11 WW/640/5w, 12 WW/512/4w global nodes,
-    //                                14 if-if/512/4w, 15 WW/768/3w, 16 WW/768/3w global nodes,
-    //                                17 WW/512/2w, 19 stats of 10
-    //   grid per image: 1 if-if, 2 WW 4w, 3 WW 5w, 4 if-if 4w, 5 WW default, 9 stats of 5
-    if (a.variant == 0 || a.variant >= 10) {
-        if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
-        size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
-        bool fits = lds <= RT_LDS_NODE_BYTES;
-        int rc;
-        switch (a.variant) {
-            case 11: rc = fits ? launch_persistent(render_persistent<true, 5, false, true, 640>, 640, lds, d, st)
-                               : launch_persistent(render_persistent<true, 5, false, false, 640>, 640, 0, d, st); break;
-            case 12: rc = launch_persistent(render_persistent<true, 4, false, false, 512>, 512, 0, d, st); break;
-            case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
-            case 31: rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<3, 4, true, false, 512>, 512, 0, d, st); break;
-            case 15: rc = fits ? launch_persistent(render_persistent<true, 3, false, true, 768>, 768, lds, d, st)
-                               : launch_persistent(render_persistent<true, 3, false, false, 768>, 768, 0, d, st); break;
-            case 16: rc = launch_persistent(render_persistent<true, 3, false, false, 768>, 768, 0, d, st); break;
-            case 17: rc = fits ? launch_persistent(render_persistent<true, 2, false, true, 512>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<true, 2, false, false, 512>, 512, 0, d, st); break;
-            case 14: rc = fits ? launch_persistent(render_persistent<false, 4, false, true, 512>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<false, 4, false, false, 512>, 512, 0, d, st); break;
-            case 19: rc = fits ? launch_persistent(render_persistent<true, 4, true, true, 512>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<true, 4, true, false, 512>, 512, 0, d, st); break;
-            case 20: rc = fits ? launch_persistent(render_persistent<true, 4, false, true, 512, true>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<true, 4, false, false, 512, true>, 512, 0, d, st); break;
-            case 21: rc = launch_persistent(render_persistent<true, 4, false, false, 512, true>, 512, 0, d, st); break;
-            case 22: rc = fits ? launch_persistent(render_persistent<true, 1, false, true, 512, true>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<true, 1, false, false, 512, true>, 512, 0, d, st); break;
-            case 23: rc = fits ? launch_persistent(render_persistent<true, 4, false, true, 1024, true>, 1024, lds, d, st)
-                               : launch_persistent(render_persistent<true, 4, false, false, 1024, true>, 1024, 0, d, st); break;
-            case 29: rc = fits ? launch_persistent(render_persistent<true, 4, true, true, 512, true>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<true, 4, true, false, 512, true>, 512, 0, d, st); break;
-            case 10: rc = fits ? launch_persistent(render_persistent<1, 4, false, true, 512>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<1, 4, false, false, 512>, 512, 0, d, st); break;
-            default: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
-                               : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
-        }
-        if (rc) return rc;
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-    dim3 block(16, 16);
-    dim3 grid((a.width + 15) / 16, (a.local_rows + 15) / 16);
+    //   0 = 30: while-while, fast slab, branch-free node step, 512 threads / 4 waves per SIMD
+    //   31 stats of 30;  10 while-while (exact slab) 512/4w;  19 stats of 10
+    //   12 = 30 with global-memory nodes;  15 = 30 at 768 threads / 3 waves
+    if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
+    size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
+    bool fits = lds <= RT_LDS_NODE_BYTES;
+    int rc;
     switch (a.variant) {
-        case 1: hipLaunchKernelGGL((render_kernel<false, 1, false>), grid, block, 0, st, d); break;
-        case 2: hipLaunchKernelGGL((render_kernel<true, 4, false>), grid, block, 0, st, d); break;
-        case 3: hipLaunchKernelGGL((render_kernel<true, 5, false>), grid, block, 0, st, d); break;
-        case 4: hipLaunchKernelGGL((render_kernel<false, 4, false>), grid, block, 0, st, d); break;
-        case 9: hipLaunchKernelGGL((render_kernel<true, 1, true>), grid, block, 0, st, d); break;
-        default: hipLaunchKernelGGL((render_kernel<true, 1, false>), grid, block, 0, st, d); break;
+        case 10: rc = fits ? launch_persistent(render_persistent<1, 4, false, true, 512>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<1, 4, false, false, 512>, 512, 0, d, st); break;
+        case 19: rc = fits ? launch_persistent(render_persistent<1, 4, true, true, 512>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<1, 4, true, false, 512>, 512, 0, d, st); break;
+        case 12: rc = launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
+        case 15: rc = fits ? launch_persistent(render_persistent<3, 3, false, true, 768>, 768, lds, d, st)
+                           : launch_persistent(render_persistent<3, 3, false, false, 768>, 768, 0, d, st); break;
+        case 31: rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<3, 4, true, false, 512>, 512, 0, d, st); break;
+        default: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
+    }
+    if (rc) return rc;
+    if (a.samples) {
+        unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);
+        hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), 0, st, d);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -129,6 +129,55 @@ def schedule_b(lanes, K):
     return np.array([ni, nl, li, ll, si, sl], float)
 
 
+def schedule_s(lanes, K, Q, stop="all"):
+    """Speculative walk (leaves queued, up to Q per lane; inner nodes may be
+    tested with a stale ray_t.max, leaves re-tested exactly when popped) plus
+    decoupled shading at >= K waiting lanes.  Node sequences are the exact
+    ones (the stale-tmax superset is not modelled)."""
+    n = len(lanes)
+    tr = [0] * n
+    ptr = np.zeros(n, int)
+    q = np.zeros(n, int)              # queued leaves
+    state = np.zeros(n, int)          # 0 traversing, 1 waiting to shade, 2 done
+    for i in range(n):
+        if not lanes[i]:
+            state[i] = 2
+    ni = nl = li = ll = si = sl = 0
+    while (state != 2).any():
+        while True:
+            trav = state == 0
+            walking = trav & (ptr < np.array([len(lanes[i][tr[i]]) if state[i] != 2 else 0 for i in range(n)]))
+            if stop == "all":   # step until every traversing lane has a leaf queued or finished walking
+                need = walking & (q == 0)
+            else:
+                need = walking & (q < Q)
+            if not need.any():
+                break
+            act = walking & (q < Q)
+            ni += 1
+            nl += int(act.sum())
+            for i in np.nonzero(act)[0]:
+                if lanes[i][tr[i]][ptr[i]]:
+                    q[i] += 1
+                ptr[i] += 1
+        if (q > 0).any():
+            li += 1
+            ll += int((q > 0).sum())
+            q[q > 0] -= 1
+        for i in range(n):
+            if state[i] == 0 and q[i] == 0 and ptr[i] >= len(lanes[i][tr[i]]):
+                state[i] = 1
+        waiting = state == 1
+        if waiting.sum() >= K or (not (state == 0).any() and waiting.any()):
+            si += 1
+            sl += int(waiting.sum())
+            for i in np.nonzero(waiting)[0]:
+                tr[i] += 1
+                ptr[i] = 0
+                state[i] = 0 if tr[i] < len(lanes[i]) else 2
+    return np.array([ni, nl, li, ll, si, sl], float)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", type=int, default=8)
@@ -148,6 +197,8 @@ def main():
     Ks = [int(k) for k in a.K.split(",")]
     A = np.zeros(6)
     B = {k: np.zeros(6) for k in Ks}
+    SQ = [(k, qd, st) for k in (64, 32, 16) for qd in (1, 2, 3, 4) for st in ("all", "full")]
+    S = {c: np.zeros(6) for c in SQ}
     for _ in range(a.tiles):
         tx, ty = int(rng.integers(0, W // 8)), int(rng.integers(0, H // 8))
         args = (ctypes.byref(osc.desc), W, H, tx * 8, tx * 8 + 8, ty * 8, ty * 8 + 8, 1, a.frames,
@@ -159,11 +210,13 @@ def main():
         A += schedule_a(lanes)
         for k in Ks:
             B[k] += schedule_b(lanes, k)
+        for c in SQ:
+            S[c] += schedule_s(lanes, *c)
     ni, nl, li, ll, si, sl = A
     # calibrate per-iteration costs on A: node 48 %, leaf 35 %, shade 12.6 % of cycles
-    cn = 0.48 / ni
-    cl = 0.35 / li
-    cs = 0.126 / si
+    cn = 0.419 / ni
+    cl = 0.39 / li
+    cs = 0.143 / si
     base = ni * cn + li * cl + si * cs
     print(f"scene {a.scene}, {a.tiles} tiles x {a.frames} frames")
     print(f"A: node it {ni:.0f} util {nl / ni / 64:.2f} | leaf it {li:.0f} util {ll / li / 64:.2f} | "
@@ -173,6 +226,12 @@ def main():
         cost = ni2 * cn + li2 * cl + si2 * cs
         print(f"B K={k:2d}: node it {ni2:.0f} util {nl2 / ni2 / 64:.2f} | leaf it {li2:.0f} util {ll2 / li2 / 64:.2f} | "
               f"shade it {si2:.0f} util {sl2 / si2 / 64:.2f} | predicted time {cost / base:.3f} x A")
+
+    for c in SQ:
+        ni2, nl2, li2, ll2, si2, sl2 = S[c]
+        cost = ni2 * cn + li2 * cl + si2 * cs
+        print(f"S K={c[0]:2d} Q={c[1]} stop={c[2]:4s}: node it {ni2:.0f} util {nl2 / ni2 / 64:.2f} | leaf it {li2:.0f} "
+              f"util {ll2 / li2 / 64:.2f} | shade it {si2:.0f} util {sl2 / si2 / 64:.2f} | predicted {cost / base:.3f} x A")
 
 
 if __name__ == "__main__":

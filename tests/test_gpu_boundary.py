@@ -137,17 +137,21 @@ def test_bound_torch_image_and_stream(gpu):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
-VARIANTS = [1, 2, 3, 4, 5, 10, 11, 12, 14, 15, 16, 17, 20, 21, 22, 23, 30]
+VARIANTS = [0, 10, 12, 15, 30]
 
 
-def test_all_kernel_variants_identical(gpu, monkeypatch):
-    """Every launch shape of the kernel (RT_KERNEL_VARIANT, used for A/B timing) renders the same bits."""
+@pytest.mark.parametrize("chunk_target", ["0", "1", "16", "100000"])
+def test_all_kernel_variants_identical(gpu, monkeypatch, chunk_target):
+    """Every launch shape of the kernel (RT_KERNEL_VARIANT, used for A/B timing) and
+    every work split (RT_CHUNK_TARGET: 0 = direct running mean in registers, else
+    tile x frame-chunk units with the fold epilogue) renders the same bits."""
     s = rtamd.Scene(8, 40, 24, seed=1)
-    ref = oracle_image(s, 4)
+    ref = oracle_image(s, 6)
+    monkeypatch.setenv("RT_CHUNK_TARGET", chunk_target)
     for v in VARIANTS:
         monkeypatch.setenv("RT_KERNEL_VARIANT", str(v))
-        out = gpu_image(s, 4)
-        assert bit_equal(out, ref), f"variant {v}: {mismatch_report(out, ref)}"
+        out = gpu_image(s, 6)
+        assert bit_equal(out, ref), f"variant {v}, chunk target {chunk_target}: {mismatch_report(out, ref)}"
 
 
 def test_stats_build_renders_same_bits(gpu):

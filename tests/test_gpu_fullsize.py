@@ -1,0 +1,87 @@
+"""Parity at BASELINE.json's full sizes (configs C2-C5), through the C ABI.
+
+The oracle cannot render a whole 1080p/4K image in seconds, so each case renders
+the full image on the GPU and checks it three ways:
+  * sampled rows: the oracle renders a few whole 8-row stripes of the same image
+    (its stripe partition: world = n_stripes, rank = stripe) and those rows must
+    match the GPU image bit for bit;
+  * work-split independence: the direct launch (running mean in registers) and
+    the tile x frame-chunk launch (per-frame colours + fold) give the same bits;
+  * partition independence: N stripe-partitioned contexts (one per rank, as
+    one process per GPU would run them) reassemble to the 1-context image.
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+import rtamd
+from helpers import bit_equal, mismatch_report
+
+pytestmark = pytest.mark.gpu
+
+STRIPE = 8
+
+
+def render(scene, frames, depth, spp, rank=0, world=1, stripe=16, chunk_target=None, monkeypatch=None):
+    if chunk_target is not None:
+        monkeypatch.setenv("RT_CHUNK_TARGET", str(chunk_target))
+    ctx = rtamd.RenderContext(devices=(0,), rank=rank, world=world, stripe_rows=stripe)
+    ctx.upload_scene(scene)
+    ctx.set_params(max_depth=depth, spp=spp)
+    ctx.resize(scene.width, scene.height)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, frames))
+    img = ctx.read_image()
+    ctx.close()
+    return img
+
+
+def oracle_rows(scene, frames, depth, spp, stripes):
+    """Oracle render of the given 8-row stripes only (rest of the image stays 0)."""
+    o = pyoracle.OracleScene(scene, max_depth=depth, spp=spp)
+    rf = rtamd.frame_rand_factors(1, 0, frames)
+    n_stripes = (scene.height + STRIPE - 1) // STRIPE
+    img = np.zeros((scene.height, scene.width, 4), np.float32)
+    for s in stripes:
+        pyoracle.render(o, rf, image=img, rank=s, world=n_stripes, stripe_rows=STRIPE)
+    return img
+
+
+def check_rows(gpu_img, ref, stripes, h):
+    for s in stripes:
+        r0, r1 = s * STRIPE, min(h, (s + 1) * STRIPE)
+        assert bit_equal(gpu_img[r0:r1], ref[r0:r1]), f"rows {r0}-{r1}: {mismatch_report(gpu_img[r0:r1], ref[r0:r1])}"
+
+
+# (config, scene, W, H, frames, spp uniform, depth)
+CONFIGS = [
+    ("C2 scene0 1080p", 0, 1920, 1080, 3, 1024, 5),
+    ("C3 scene8 1080p", 8, 1920, 1080, 3, 4096, 5),
+    ("C4 scene6 1080p", 6, 1920, 1080, 3, 4096, 5),
+    ("C5 scene8 4K", 8, 3840, 2160, 2, 8192, 5),
+]
+
+
+@pytest.mark.parametrize("name,sid,w,h,frames,spp,depth", CONFIGS, ids=[c[0] for c in CONFIGS])
+def test_full_size_sampled_rows_match_oracle(gpu, monkeypatch, name, sid, w, h, frames, spp, depth):
+    scene = rtamd.Scene(sid, w, h, seed=1)
+    n_stripes = (h + STRIPE - 1) // STRIPE
+    rng = np.random.default_rng(sid * 7 + w)
+    stripes = sorted({0, n_stripes - 1, *rng.choice(n_stripes, 3, replace=False).tolist()})
+    direct = render(scene, frames, depth, spp, chunk_target=0, monkeypatch=monkeypatch)
+    chunked = render(scene, frames, depth, spp, chunk_target=64, monkeypatch=monkeypatch)
+    assert bit_equal(direct, chunked), "direct vs chunked: " + mismatch_report(direct, chunked)
+    ref = oracle_rows(scene, frames, depth, spp, stripes)
+    check_rows(direct, ref, stripes, h)
+    assert np.isfinite(direct[..., 3]).all() and (direct[..., 3] == 1.0).all()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_full_size_stripe_partition_equals_one_gpu(gpu, world):
+    """BASELINE C5's tile partition: the N-rank stripes reassemble to the 1-rank image."""
+    scene = rtamd.Scene(8, 1920, 1080, seed=1)
+    one = render(scene, 2, 5, 8192)
+    parts = np.stack([
+        np.pad(blk, ((0, rtamd.padded_local_rows(1080, world, STRIPE) - blk.shape[0]), (0, 0), (0, 0)))
+        for blk in (render(scene, 2, 5, 8192, rank=r, world=world, stripe=STRIPE) for r in range(world))])
+    full = rtamd.deinterleave(parts, 1080, world, STRIPE)
+    assert bit_equal(full, one), mismatch_report(full, one)

@@ -2,7 +2,9 @@
 
 Every variant must produce the same bits; timings are HIP-event device time of
 one rt_render call (1 launch) per round, reported as median/min over rounds.
-usage: python tools/ab_variants.py [--variants 0,1,2] [--rounds 5] [--scene 8]
+A variant spec is "<RT_KERNEL_VARIANT>" or "<variant>c<RT_CHUNK_TARGET>" (e.g. 30c0 =
+variant 30 with the direct, unchunked work split).
+usage: python tools/ab_variants.py [--variants 30c0,30c16] [--rounds 5] [--scene 8]
 """
 import argparse
 import os
@@ -17,7 +19,10 @@ import rtamd  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2,3,4")
+    ap.add_argument("--variants", default="30c0,30c16")
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--stripe-rows", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--scene", type=int, default=8)
     ap.add_argument("--width", type=int, default=1920)
@@ -25,12 +30,17 @@ def main():
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--depth", type=int, default=5)
     a = ap.parse_args()
-    variants = [int(v) for v in a.variants.split(",")]
+    variants = a.variants.split(",")
     scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
     ctxs = {}
     for v in variants:
-        os.environ["RT_KERNEL_VARIANT"] = str(v)
-        c = rtamd.RenderContext(devices=(0,))
+        kv, _, ct = v.partition("c")
+        os.environ["RT_KERNEL_VARIANT"] = kv
+        if ct:
+            os.environ["RT_CHUNK_TARGET"] = ct
+        else:
+            os.environ.pop("RT_CHUNK_TARGET", None)
+        c = rtamd.RenderContext(devices=(0,), rank=a.rank, world=a.world, stripe_rows=a.stripe_rows)
         c.upload_scene(scene)
         c.set_params(max_depth=a.depth, spp=4096)
         c.resize(a.width, a.height)
@@ -55,7 +65,7 @@ def main():
                     print(f"variant {v}: bits {'identical' if same else 'DIFFER'} to variant {variants[0]}")
                 continue
             times[v].append(ns / 1e6)
-    samples = a.width * a.height * a.frames
+    samples = a.width * rtamd.local_rows(a.height, a.rank, a.world, a.stripe_rows) * a.frames
     for v in variants:
         med = statistics.median(times[v])
         print(f"variant {v}: median {med:.2f} ms  min {min(times[v]):.2f} ms  -> {samples / med / 1e3:.1f} Msamples/s")
