@@ -104,10 +104,12 @@ def main():
     import rtamd
     from rtamd import dist as rdist
 
-    rank, world, local_rank = rdist.init_from_env()
+    # RT_BENCH_BACKEND=gloo RT_BENCH_DEVICE=0: rehearse the N-rank path with every
+    # rank on one GPU (gloo collectives); the driver's real N-GPU runs use RCCL.
+    rank, world, local_rank = rdist.init_from_env(os.environ.get("RT_BENCH_BACKEND"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    dev = local_rank
+    dev = int(os.environ.get("RT_BENCH_DEVICE", local_rank))
     torch.cuda.set_device(dev)
     stream = torch.cuda.Stream(device=dev)
 
@@ -157,7 +159,8 @@ def main():
     launches_per_step = math.ceil(F / 256)
     t_max = elapsed
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        on_gpu = torch.distributed.get_backend() == "nccl"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}" if on_gpu else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         t_max = float(t.item())
 

@@ -34,6 +34,7 @@ struct Device {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     bool timed = false;
     DevBuf nodes, spheres, quads, boxes, media, lights, tex[8];
+    DevBuf dquads, dboxes;   // intersection-only face records (rt_device.h)
     DevBuf image;            // internal image
     DevBuf args;             // rt_kernel_args slot in device memory
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
@@ -66,6 +67,8 @@ struct rt_ctx {
     int width = 0, height = 0;
     int proc_rank = 0, proc_world = 1, stripe_rows = 16;
     int n_dnodes = 0;
+    bool spec_ok = false;   // every child box lies inside its parent's (speculative walk allowed)
+    int shade_k = 32;       // decoupled schedule threshold (env RT_SHADE_K)
     bool uv_always = false;
     bool validated = false;
     uint64_t last_ns = 0;
@@ -219,6 +222,44 @@ int thread_bvh(rt_ctx* c, const rt_bvh_node* in, int n, std::vector<rt_dnode>& o
     return RT_OK;
 }
 
+// Every inner node's two children (right = k+1, left = skip of k+1) lie inside
+// its box.  The reference's builder guarantees it (a node's box is the padded
+// join of its children's, AABB.java:15-66); uploaded bytes are checked anyway
+// because the speculative walk (rt_kernel.hip, Trace) relies on it.
+bool boxes_nest(const std::vector<rt_dnode>& dn) {
+    const int m = (int)dn.size();
+    auto inside = [](const rt_dnode& c, const rt_dnode& p) {
+        return c.xmin >= p.xmin && c.xmax <= p.xmax && c.ymin >= p.ymin && c.ymax <= p.ymax && c.zmin >= p.zmin &&
+               c.zmax <= p.zmax;
+    };
+    for (int k = 0; k < m; k++) {
+        if ((dn[k].meta & 0xF0000u) != 0) continue;   // leaf
+        if (k + 1 >= m) return false;
+        uint32_t l = dn[k + 1].meta & 0xFFFFu;
+        if (l == RT_NODE_END || (int)l >= m) return false;
+        if (!inside(dn[k + 1], dn[k]) || !inside(dn[l], dn[k])) return false;
+    }
+    return true;
+}
+
+// Intersection-only record of one quad face (rt_device.h, RT_DFACE_F4): the
+// plane (normal, d) and the 2-D Cramer system of hit_quad (hitting.glsl:90-122)
+// with its axis pair and delta precomputed by the same float expressions.
+void face_record(const rt_quad& q, float4 out[3]) {
+    const float* u = q.u;
+    const float* v = q.v;
+    float delta;
+    int a, b, cs;
+    if ((delta = u[0] * v[1] - u[1] * v[0]) != 0.0f) { a = 0; b = 1; cs = 0; }
+    else if ((delta = u[0] * v[2] - u[2] * v[0]) != 0.0f) { a = 0; b = 2; cs = 1; }
+    else { delta = u[1] * v[2] - u[2] * v[1]; a = 1; b = 2; cs = 2; }
+    float csf;
+    std::memcpy(&csf, &cs, 4);
+    out[0] = make_float4(q.normal[0], q.normal[1], q.normal[2], q.d);
+    out[1] = make_float4(q.q[a], q.q[b], u[a], u[b]);
+    out[2] = make_float4(v[a], v[b], delta, csf);
+}
+
 int validate(rt_ctx* c) {
     if (c->validated) return RT_OK;
     size_t ns = c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere);
@@ -307,6 +348,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     rt_ctx* c = new rt_ctx();
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) c->variant = std::atoi(v);
     if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("RT_SHADE_K")) c->shade_k = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
         Device& d = c->devs[i];
@@ -332,6 +374,7 @@ int rt_destroy(rt_ctx* c) {
         (void)hipStreamSynchronize(d.stream);
         dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter); dev_free(d.samples);
+        dev_free(d.dquads); dev_free(d.dboxes);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
             if (e) (void)hipEventDestroy(e);
@@ -367,9 +410,31 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
         int r = thread_bvh(c, (const rt_bvh_node*)H.data(), (int)(nbytes / sizeof(rt_bvh_node)), dn);
         if (r) return r;
         c->n_dnodes = (int)dn.size();
+        c->spec_ok = boxes_nest(dn);
         dev_bytes.assign((uint8_t*)dn.data(), (uint8_t*)dn.data() + dn.size() * sizeof(rt_dnode));
         src = dev_bytes.data();
         n = dev_bytes.size();
+    }
+    std::vector<float4> faces;   // intersection-only copy of quads / box sides
+    if (binding == RT_BIND_QUADS || binding == RT_BIND_BOXES) {
+        const rt_quad* qs = (const rt_quad*)bytes;
+        size_t nq = nbytes / sizeof(rt_quad);   // a box is 6 consecutive quads
+        faces.resize(nq * RT_DFACE_F4);
+        if (binding == RT_BIND_QUADS) {
+            for (size_t k = 0; k < nq; k++) face_record(qs[k], &faces[k * RT_DFACE_F4]);
+        } else {
+            // per box: the 6 planes first, then the 6 (A, B) pairs (RT_DBOX_F4 float4)
+            for (size_t bx = 0; bx < nq / 6; bx++) {
+                float4* o = &faces[bx * RT_DBOX_F4];
+                for (int i = 0; i < 6; i++) {
+                    float4 f[3];
+                    face_record(qs[bx * 6 + i], f);
+                    o[i] = f[0];
+                    o[6 + 2 * i] = f[1];
+                    o[7 + 2 * i] = f[2];
+                }
+            }
+        }
     }
     if (binding == RT_BIND_LIGHTS) {
         if (nbytes < 4) return set_err(c, RT_ERR_INVALID_ARG, "lights buffer needs the count word");
@@ -388,6 +453,11 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
         }
         int r = dev_alloc_copy(c, d, *b, src, n);
         if (r) return r;
+        if (binding == RT_BIND_QUADS || binding == RT_BIND_BOXES) {
+            r = dev_alloc_copy(c, d, binding == RT_BIND_QUADS ? d.dquads : d.dboxes, faces.data(),
+                               faces.size() * sizeof(float4));
+            if (r) return r;
+        }
     }
     return RT_OK;
 }
@@ -522,6 +592,8 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.lights_count = lc;
     a.uv_always = c->uv_always;
     a.variant = c->variant;
+    a.spec_ok = c->spec_ok ? 1 : 0;
+    a.shade_k = c->shade_k;
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
     a.max_depth = c->max_depth;
@@ -537,6 +609,8 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         a.spheres = (const rt_sphere*)d.spheres.ptr;
         a.quads = (const rt_quad*)d.quads.ptr;
         a.boxes = (const rt_box*)d.boxes.ptr;
+        a.dquads = (const float4*)d.dquads.ptr;
+        a.dboxes = (const float4*)d.dboxes.ptr;
         a.media = (const rt_medium*)d.media.ptr;
         a.lights = (const int32_t*)d.lights.ptr;
         for (int t = 0; t < 8; t++) {
@@ -751,7 +825,7 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
     // stats twin of the current launch shape: 0/12/15/30 -> 31, 10 -> 19
     if (on) {
         int v = c->variant;
-        c->variant = (v == 10 || v == 19) ? 19 : 31;
+        c->variant = (v == 10 || v == 19) ? 19 : (v >= 40 && v < 50) ? 49 : 31;
     } else {
         c->variant = 0;
     }

@@ -6,6 +6,9 @@
 //   spheres  : rt_sphere[] as uploaded (48 B AoS)
 //   quads    : rt_quad[]   as uploaded (80 B AoS)
 //   boxes    : rt_box[]    as uploaded (480 B AoS)
+//   dquads   : per quad RT_DFACE_F4 float4: plane (n, d), A = (q_a, q_b, u_a, u_b),
+//              B = (v_a, v_b, delta, axis case) — the intersection-only face record
+//   dboxes   : per box RT_DBOX_F4 float4: the 6 planes, then the 6 (A, B) pairs
 //   media    : rt_medium[] as uploaded (20 B)
 //   lights   : int32 packed ids
 //   textures : RGB8 expanded to RGBA8 (4 B/texel, aligned), RGBA8, R32F
@@ -20,6 +23,8 @@
 
 #define RT_MAX_FRAMES_PER_LAUNCH 256
 #define RT_NODE_END 0xFFFFu
+#define RT_DFACE_F4 3    // float4 per dquads record
+#define RT_DBOX_F4 18    // float4 per dboxes record
 #define RT_LDS_NODE_BYTES (64 * 1024)   // stage the BVH in LDS when it fits (2 workgroups/CU)
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
@@ -47,6 +52,8 @@ struct rt_kernel_args {
     const rt_sphere* spheres;
     const rt_quad* quads;
     const rt_box* boxes;
+    const float4* dquads;
+    const float4* dboxes;
     const rt_medium* media;
     const int32_t* lights;
     int n_nodes, lights_count;
@@ -69,6 +76,8 @@ struct rt_kernel_args {
     int n_chunks, chunk_frames;
     float4* samples;             // chunked mode: per-frame colours [n_frames][n_pixels]; nullptr = direct
     size_t n_pixels;             // local_rows * width
+    int shade_k;                 // decoupled schedule: shade once this many lanes wait
+    int spec_ok;                 // BVH boxes nest (child inside parent): speculative walk allowed
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
 };
 

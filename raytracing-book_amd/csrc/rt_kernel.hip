@@ -109,54 +109,49 @@ __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float ti
     return true;
 }
 
-// hitting.glsl:103-124: is the plane hit at t inside the quad? (alpha, beta) out.
-__device__ __forceinline__ bool quad_interior(const float4* __restrict__ q, v3 o, v3 d, float t, float& alpha,
-                                              float& beta) {
-    float4 Q1 = q[1], Q2 = q[2], Q3 = q[3];
-    v3 inter = add3(o, scale3(d, t));
-    v3 ph = sub3(inter, f3(Q1));
-    v3 u = f3(Q2), v = f3(Q3);
-    float delta;
-    if ((delta = u.x * v.y - u.y * v.x) != 0.0f) {
-        alpha = (ph.x * v.y - ph.y * v.x) / delta;
-        beta = (ph.y * u.x - ph.x * u.y) / delta;
-    } else if ((delta = u.x * v.z - u.z * v.x) != 0.0f) {
-        alpha = (ph.x * v.z - ph.z * v.x) / delta;
-        beta = (ph.z * u.x - ph.x * u.z) / delta;
-    } else {
-        delta = u.y * v.z - u.z * v.y;
-        alpha = (ph.y * v.z - ph.z * v.y) / delta;
-        beta = (ph.z * u.y - ph.y * u.z) / delta;
-    }
+// hitting.glsl:103-124 on an intersection-only face record (rt_device.h):
+// A = (q_a, q_b, u_a, u_b), B = (v_a, v_b, delta, axis case).  The host chose
+// the reference's first non-degenerate projection (xy, xz, else yz) and
+// computed delta with the reference's expression, so alpha/beta here are the
+// reference's values: intersection = o + dir*t, ph = intersection - q, then the
+// 2-D Cramer quotients on the chosen pair of axes.
+__device__ __forceinline__ bool face_interior(float4 A, float4 B, v3 o, v3 d, float t, float& alpha, float& beta) {
+    const int cs = __float_as_int(B.w);
+    float oa = (cs == 2) ? o.y : o.x, da = (cs == 2) ? d.y : d.x;
+    float ob = (cs == 0) ? o.y : o.z, db = (cs == 0) ? d.y : d.z;
+    float pa = (oa + da * t) - A.x;
+    float pb = (ob + db * t) - A.y;
+    alpha = (pa * B.y - pb * B.x) / B.z;
+    beta = (pb * A.z - pa * A.w) / B.z;
     return (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
 
-// hitting.glsl:90-133 without the record writes.
-__device__ __forceinline__ bool quad_test(const float4* __restrict__ q, v3 o, v3 d, float tmin, float tmax, float& t,
+// hitting.glsl:90-133 without the record writes; f = dquads record.
+__device__ __forceinline__ bool quad_test(const float4* __restrict__ f, v3 o, v3 d, float tmin, float tmax, float& t,
                                           float& alpha, float& beta) {
-    float4 Q0 = q[0];
+    float4 Q0 = f[0];
     v3 n = f3(Q0);
     float denom = g_dot(n, d);
     if (fabsf(denom) < 1e-8f) return false;
     float tt = (Q0.w - g_dot(n, o)) / denom;
     if (!(tmin <= tt && tt <= tmax)) return false;
-    if (!quad_interior(q, o, d, tt, alpha, beta)) return false;
+    if (!face_interior(f[1], f[2], o, d, tt, alpha, beta)) return false;
     t = tt;
     return true;
 }
 
-// hitting.glsl:135-146.  The six faces' plane parameters t_i do not depend on
-// the shrinking ray_t.max, so they are divided independently (ILP); faces are
-// then accepted in the reference order with the reference's sequential test
-// tmin <= t_i <= current max, and only those reach the interior test — the same
-// tests on the same values, so the same result.
-__device__ __forceinline__ bool box_test(const float4* __restrict__ b, v3 o, v3 d, float tmin, float tmax, float& t,
+// hitting.glsl:135-146; fb = dboxes record.  The six faces' plane parameters
+// t_i do not depend on the shrinking ray_t.max, so they are divided
+// independently (ILP); faces are then accepted in the reference order with the
+// reference's sequential test tmin <= t_i <= current max, and only those reach
+// the interior test — the same tests on the same values, so the same result.
+__device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3 d, float tmin, float tmax, float& t,
                                          int& face, float& alpha, float& beta) {
     float ti[6];
     unsigned cand = 0;
 #pragma unroll
     for (int i = 0; i < 6; i++) {
-        float4 pl = b[5 * i];
+        float4 pl = fb[i];
         v3 n = f3(pl);
         float denom = g_dot(n, d);
         ti[i] = (pl.w - g_dot(n, o)) / denom;   // unused when |denom| < 1e-8
@@ -167,7 +162,7 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ b, v3 o, v3 
     for (int i = 0; i < 6; i++) {
         if ((cand >> i) & 1u) {
             float al, be;
-            if (ti[i] <= tmax && quad_interior(b + 5 * i, o, d, ti[i], al, be)) {
+            if (ti[i] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[i], al, be)) {
                 tmax = ti[i];
                 t = ti[i];
                 face = i;
@@ -188,9 +183,8 @@ __device__ __noinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3
     int face;
     if (type == RT_MODEL_SPHERE)
         return sphere_t(reinterpret_cast<const float4*>(P.spheres + idx), time, o, d, a, tmin, tmax, t);
-    if (type == RT_MODEL_QUAD) return quad_test(reinterpret_cast<const float4*>(P.quads + idx), o, d, tmin, tmax, t, al, be);
-    if (type == RT_MODEL_BOX)
-        return box_test(reinterpret_cast<const float4*>(P.boxes + idx), o, d, tmin, tmax, t, face, al, be);
+    if (type == RT_MODEL_QUAD) return quad_test(P.dquads + RT_DFACE_F4 * idx, o, d, tmin, tmax, t, al, be);
+    if (type == RT_MODEL_BOX) return box_test(P.dboxes + RT_DBOX_F4 * idx, o, d, tmin, tmax, t, face, al, be);
     return false;
 }
 
@@ -311,10 +305,10 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
             hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t);
             if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
         } else if (ty == RT_MODEL_QUAD) {
-            hit = quad_test(reinterpret_cast<const float4*>(P.quads + ix), o, d, tmin, tmax, t, al, be);
+            hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, tmax, t, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_BOX) {
-            hit = box_test(reinterpret_cast<const float4*>(P.boxes + ix), o, d, tmin, tmax, t, face, al, be);
+            hit = box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
             hit = medium_test(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
@@ -588,7 +582,7 @@ __device__ __forceinline__ float sphere_light_pdf(const KP& P, int idx, v3 o, v3
 __device__ __forceinline__ float quad_light_pdf(const KP& P, int idx, v3 o, v3 d) {
     const float4* q = reinterpret_cast<const float4*>(P.quads + idx);
     float t, al, be;
-    if (!quad_test(q, o, d, 0.001f, RT_INFINITY, t, al, be)) return 0.0f;
+    if (!quad_test(P.dquads + RT_DFACE_F4 * idx, o, d, 0.001f, RT_INFINITY, t, al, be)) return 0.0f;
     v3 n = f3(q[0]);
     bool front = g_dot(d, n) < 0.0f;
     v3 normal = front ? n : neg3(n);
@@ -892,6 +886,220 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
     if (direct) *px = prev;
 }
 
+// ---------------------------------------------------------------------------
+// Decoupled schedule (variant 40+): a lane's trace state lives across the
+// wave's stages, so lanes whose trace ended wait for shading while the others
+// keep walking, and the wave shades once >= P.shade_k lanes wait (or no lane is
+// walking).  Within a trace, lanes with finite 1/dir keep walking past a hit
+// leaf ("speculative" walk) and queue up to Q leaves; the queue is drained in
+// order, one leaf per lane per leaf stage.
+//
+// Why a walk past a pending leaf stays exact: a queued leaf's prims may shrink
+// ray_t.max, so the inner nodes tested meanwhile saw a stale (larger) max.  The
+// reference visits leaf L iff L's AABB passes at the max current when L is
+// popped (its ancestors then pass too: child boxes lie inside their parent's
+// box, AABB.java join/pad only grow, and with finite 1/dir the slab interval
+// is monotone in the box bounds and in ray_t.max).  A larger max only admits
+// more inner nodes, so the walk enumerates a superset of the reference's
+// leaves in the reference's pre-order, and every leaf's AABB is re-tested
+// exactly with the current max when it is dequeued.  Media draw rand() only in
+// the leaf stage, in that same order.  The host checks the box nesting on
+// upload (P.spec_ok); rays with an infinite 1/dir component never speculate.
+struct Trace {
+    Hit h;
+    v3 inv;
+    float a, tmax;
+    uint32_t ni;      // next node of the walk (RT_NODE_END: walk finished)
+    uint64_t q;       // queued leaf nodes, 16 bits each, head in the low bits
+    int qn;           // queue length
+    bool has;
+    bool exact;       // 1/dir has a -inf component: exact slab semantics
+    bool spec;        // may walk past a queued leaf
+};
+
+// compute.glsl:304-306 + trace_through_bvh's prologue (:226-236) for S's ray.
+// Returns false when the loop bound ends the sample (final_color stays 0).
+__device__ __forceinline__ bool begin_trace(const KP& P, Path& S, Trace& T) {
+    if (S.depth >= P.max_depth) return false;
+    S.depth++;
+    v3 d = S.d;
+    T.h.t = 0.0f; T.h.type = 0; T.h.idx = 0; T.h.face = 0;
+    T.h.uv_kind_idx = 0; T.h.uv_a = 0.0f; T.h.uv_b = 0.0f;
+    T.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    T.a = g_dot(d, d);
+    T.tmax = RT_INFINITY;
+    T.has = false;
+    T.q = 0;
+    T.qn = 0;
+    // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
+    bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
+    T.ni = (dir_zero || P.n_nodes == 0) ? RT_NODE_END : 0u;
+    T.exact = (T.inv.x == -INFINITY) || (T.inv.y == -INFINITY) || (T.inv.z == -INFINITY);
+    T.spec = P.spec_ok && fabsf(T.inv.x) < INFINITY && fabsf(T.inv.y) < INFINITY && fabsf(T.inv.z) < INFINITY;
+    return true;
+}
+
+// The node at T.ni (compute.glsl:237-262): inner hit -> its right child
+// (T.ni + 1), leaf hit -> queued, anything else -> the skip link.
+__device__ __forceinline__ void node_step(const float4* __restrict__ nodes, Trace& T, v3 o, bool wave_exact) {
+    const uint32_t i = T.ni;
+    float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
+    uint32_t meta = __float_as_uint(n1.z);
+    bool hitn;
+    if (!wave_exact) {
+        hitn = aabb_fast(n0, n1, o, T.inv, 0.001f, T.tmax);
+    } else {
+        float lo = 0.001f, hi = T.tmax;
+        slab(n0.x, n0.y, o.x, T.inv.x, lo, hi);
+        slab(n0.z, n0.w, o.y, T.inv.y, lo, hi);
+        slab(n1.x, n1.y, o.z, T.inv.z, lo, hi);
+        hitn = !(hi <= lo);
+    }
+    bool inner = (meta & 0xF0000u) == 0;
+    T.ni = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
+    if (hitn && !inner) {
+        T.q |= (uint64_t)i << (16 * T.qn);
+        T.qn++;
+    }
+}
+
+// Dequeue the head leaf, re-test its AABB with the current ray_t.max and, on a
+// hit, test its two prims (compute.glsl:247-256).
+template <bool STATS>
+__device__ __forceinline__ void leaf_stage(const KP& P, const float4* __restrict__ nodes, Path& S, Trace& T, float px,
+                                           float py, unsigned long long* st) {
+    const uint32_t i = (uint32_t)(T.q & 0xFFFFu);
+    T.q >>= 16;
+    T.qn--;
+    float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
+    bool hitn;
+    if (!T.exact) {
+        hitn = aabb_fast(n0, n1, S.o, T.inv, 0.001f, T.tmax);
+    } else {
+        float lo = 0.001f, hi = T.tmax;
+        slab(n0.x, n0.y, S.o.x, T.inv.x, lo, hi);
+        slab(n0.z, n0.w, S.o.y, T.inv.y, lo, hi);
+        slab(n1.x, n1.y, S.o.z, T.inv.z, lo, hi);
+        hitn = !(hi <= lo);
+    }
+    if (hitn)
+        leaf_prims<STATS>(P, __float_as_uint(n1.z), __float_as_uint(n1.w), S.o, S.d, T.a, S.time, 0.001f, T.tmax, S.rf,
+                          px, py, T.h, T.has, st);
+}
+
+template <int Q, bool STATS>
+__device__ __forceinline__ void render_pixel_dec(const KP& P, const float4* __restrict__ nodes, int x, int lr, int f0,
+                                                 int f1, bool valid, unsigned long long* st) {
+    int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
+    int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
+    const size_t pix = (size_t)lr * P.width + x;
+    float4* px = reinterpret_cast<float4*>(P.image) + pix;
+    const bool direct = P.samples == nullptr;
+    float4 prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (valid && direct) prev = *px;
+    const rt_camera_ubo& C = P.cam;
+    float fx = (float)x, fy = (float)y;
+    v3 base = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
+    Path S;
+    Trace T;
+    int f = f0;
+    // 0: start the next frame, 1: tracing, 2: trace done (shade pending), 3: all frames done
+    int state = (valid && f < f1) ? 0 : 3;
+    for (;;) {
+        // ---- start paths (a path can end at once when max_depth <= 0)
+        while (state == 0) {
+            unsigned long long t0 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
+            start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, base);
+            if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
+            if (begin_trace(P, S, T)) {
+                state = 1;
+            } else {
+                v3 cur = mk3s(0.0f);
+                if (direct) {
+                    int fc = P.first_frame + f;
+                    float n1 = (float)(fc - 1), n = (float)fc;
+                    prev.x = (prev.x * n1 + cur.x) / n;
+                    prev.y = (prev.y * n1 + cur.y) / n;
+                    prev.z = (prev.z * n1 + cur.z) / n;
+                    prev.w = 1.0f;
+                } else {
+                    P.samples[(size_t)f * P.n_pixels + pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                }
+                f++;
+                state = (f < f1) ? 0 : 3;
+            }
+        }
+        // ---- traversal stages until enough lanes wait for shading
+        for (;;) {
+            const bool wave_exact = __ballot(state == 1 && T.exact) != 0;   // uniform
+            unsigned long long t0 = STATS ? clock64() : 0;
+            for (;;) {
+                bool walking = state == 1 && T.ni != RT_NODE_END;
+                bool need = walking && T.qn == 0;
+                if (__ballot(need) == 0) break;
+                bool want = walking && (T.qn == 0 || (T.spec && T.qn < Q));
+                if (STATS) st_pred(st, want, ST_NODE_IT, ST_NODE_LN);
+                if (want) node_step(nodes, T, S.o, wave_exact);
+            }
+            if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
+            bool pend = state == 1 && T.qn > 0;
+            if (__ballot(pend) != 0) {
+                unsigned long long t1 = STATS ? clock64() : 0;
+                if (STATS) st_pred(st, pend, ST_LEAF_IT, ST_LEAF_LN);
+                if (pend) leaf_stage<STATS>(P, nodes, S, T, fx, fy, st);
+                if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+            }
+            if (state == 1 && T.ni == RT_NODE_END && T.qn == 0) state = 2;
+            unsigned long long m_wait = __ballot(state == 2);
+            if (__popcll(m_wait) >= P.shade_k || __ballot(state == 1) == 0) break;
+        }
+        // ---- shading (the rest of ray_color's loop body, compute.glsl:307-340)
+        if (state == 2) {
+            unsigned long long ts = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
+            const Hit& h = T.h;
+            if (h.uv_kind_idx != 0) {
+                bool sph = (h.uv_kind_idx >> 16) == 1;
+                v3 up = add3(S.o, scale3(S.d, h.uv_a));
+                S.uvs.kind_idx = h.uv_kind_idx;
+                S.uvs.a = sph ? up.x : h.uv_a;
+                S.uvs.b = sph ? up.y : h.uv_b;
+                S.uvs.c = sph ? up.z : S.uvs.c;
+            }
+            v3 cur;
+            bool done;
+            if (!T.has) {
+                cur = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
+                done = true;
+            } else {
+                done = shade(P, S, h, fx, fy, cur);
+            }
+            if (!done) {
+                if (begin_trace(P, S, T)) state = 1;
+                else { cur = mk3s(0.0f); done = true; }
+            }
+            if (done) {
+                if (direct) {
+                    int fc = P.first_frame + f;
+                    float n1 = (float)(fc - 1), n = (float)fc;
+                    prev.x = (prev.x * n1 + cur.x) / n;
+                    prev.y = (prev.y * n1 + cur.y) / n;
+                    prev.z = (prev.z * n1 + cur.z) / n;
+                    prev.w = 1.0f;
+                } else {
+                    P.samples[(size_t)f * P.n_pixels + pix] = make_float4(cur.x, cur.y, cur.z, 0.0f);
+                }
+                f++;
+                state = (f < f1) ? 0 : 3;
+            }
+            if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
+        }
+        if (__ballot(state != 3) == 0) break;
+    }
+    if (valid && direct) *px = prev;
+}
+
 // Persistent kernel: one resident grid; each workgroup stages the threaded BVH
 // (32 B/node, 57 KB for scene 8) in LDS once, then each wave repeatedly takes
 // the next work unit from a device-wide counter (one returning atomic per
@@ -899,7 +1107,7 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
 // reaches.  A unit is one 8x8 pixel tile x one chunk of the launch's frames
 // (unit = chunk * n_tiles + tile), so a launch over few tiles (a narrow stripe
 // set at N GPUs) still has many more units than resident waves.
-template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK>
+template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
@@ -931,7 +1139,13 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         const int f1 = min(P.n_frames, f0 + P.chunk_frames);
         int x = (tile % tiles_x) * 8 + (lane & 7);
         int lr = (tile / tiles_x) * 8 + (lane >> 3);
-        if (x < P.width && lr < P.local_rows) {
+        if (DECQ > 0) {
+            // every lane enters (the stages are wave-wide); invalid lanes idle
+            bool valid = x < P.width && lr < P.local_rows;
+            int xc = valid ? x : 0, lc = valid ? lr : 0;
+            if (LDSN) render_pixel_dec<DECQ, STATS>(P, s_nodes, xc, lc, f0, f1, valid, st);
+            else render_pixel_dec<DECQ, STATS>(P, reinterpret_cast<const float4*>(P.nodes), xc, lc, f0, f1, valid, st);
+        } else if (x < P.width && lr < P.local_rows) {
             if (LDSN) render_pixel<WW, STATS>(P, s_nodes, x, lr, f0, f1, st);
             else render_pixel<WW, STATS>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, f0, f1, st);
         }
@@ -1031,6 +1245,14 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
         case 12: rc = launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
         case 15: rc = fits ? launch_persistent(render_persistent<3, 3, false, true, 768>, 768, lds, d, st)
                            : launch_persistent(render_persistent<3, 3, false, false, 768>, 768, 0, d, st); break;
+        case 41: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 1>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<3, 4, false, false, 512, 1>, 512, 0, d, st); break;
+        case 42: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 2>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<3, 4, false, false, 512, 2>, 512, 0, d, st); break;
+        case 43: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 3>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<3, 4, false, false, 512, 3>, 512, 0, d, st); break;
+        case 49: rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512, 2>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<3, 4, true, false, 512, 2>, 512, 0, d, st); break;
         case 31: rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512>, 512, lds, d, st)
                            : launch_persistent(render_persistent<3, 4, true, false, 512>, 512, 0, d, st); break;
         default: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)

@@ -45,7 +45,8 @@ def gather_image(local_block, height, world, stripe_rows):
         dist.all_gather_into_tensor(out, local_block.contiguous())
         g = out.cpu().numpy()
     else:
-        parts = [torch.empty_like(local_block) for _ in range(world)]
-        dist.all_gather(parts, local_block.contiguous())
+        blk = local_block.detach().cpu().contiguous()   # gloo gathers host tensors
+        parts = [torch.empty_like(blk) for _ in range(world)]
+        dist.all_gather(parts, blk)
         g = np.stack([p.cpu().numpy() for p in parts])
     return deinterleave(g, height, world, stripe_rows)

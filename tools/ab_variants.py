@@ -2,8 +2,9 @@
 
 Every variant must produce the same bits; timings are HIP-event device time of
 one rt_render call (1 launch) per round, reported as median/min over rounds.
-A variant spec is "<RT_KERNEL_VARIANT>" or "<variant>c<RT_CHUNK_TARGET>" (e.g. 30c0 =
-variant 30 with the direct, unchunked work split).
+A variant spec is "<RT_KERNEL_VARIANT>" optionally followed by c<RT_CHUNK_TARGET>
+and/or k<RT_SHADE_K> (e.g. 30c0 = variant 30 with the direct, unchunked work
+split; 42k16 = variant 42 shading once 16 lanes wait).
 usage: python tools/ab_variants.py [--variants 30c0,30c16] [--rounds 5] [--scene 8]
 """
 import argparse
@@ -34,12 +35,15 @@ def main():
     scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
     ctxs = {}
     for v in variants:
-        kv, _, ct = v.partition("c")
-        os.environ["RT_KERNEL_VARIANT"] = kv
-        if ct:
-            os.environ["RT_CHUNK_TARGET"] = ct
-        else:
-            os.environ.pop("RT_CHUNK_TARGET", None)
+        import re
+        m = re.fullmatch(r"(\d+)(?:c(\d+))?(?:k(\d+))?", v)
+        assert m, f"bad variant spec {v}"
+        os.environ["RT_KERNEL_VARIANT"] = m.group(1)
+        for env, val in (("RT_CHUNK_TARGET", m.group(2)), ("RT_SHADE_K", m.group(3))):
+            if val:
+                os.environ[env] = val
+            else:
+                os.environ.pop(env, None)
         c = rtamd.RenderContext(devices=(0,), rank=a.rank, world=a.world, stripe_rows=a.stripe_rows)
         c.upload_scene(scene)
         c.set_params(max_depth=a.depth, spp=4096)

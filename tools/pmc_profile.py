@@ -25,6 +25,12 @@ GROUPS = [
     ["GRBM_GUI_ACTIVE", "GRBM_COUNT"],
     ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_SCRATCH" if False else "SQ_INSTS_FLAT"],
     ["SQ_WAIT_INST_LDS", "SQ_INSTS_BRANCH", "SQ_INST_CYCLES_VMEM", "SQ_ACTIVE_INST_SCA"],
+    ["TA_TA_BUSY_sum", "TA_FLAT_READ_WAVEFRONTS_sum", "GRBM_GUI_ACTIVE"],
+    ["TD_TD_BUSY", "TD_TC_STALL"],
+    ["SQ_ACTIVE_INST_VMEM", "SQ_INST_CYCLES_VMEM_RD", "SQ_BUSY_CU_CYCLES", "SQ_INST_LEVEL_VMEM",
+     "SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL"],
+    ["TCP_PENDING_STALL_CYCLES_sum", "TCP_TCR_RDRET_STALL_sum", "TCP_READ_TAGCONFLICT_STALL_CYCLES_sum",
+     "TCP_TCP_TA_DATA_STALL_CYCLES_sum"],
 ]
 
 
