@@ -40,6 +40,8 @@ struct Device {
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
     DevBuf counter;          // persistent-kernel work-unit counter
     DevBuf samples;          // chunked launches: per-frame colours
+    DevBuf wf_q[2], wf_hits, wf_ctr;   // wavefront pipeline (variant 50)
+    unsigned* wf_host_ctr = nullptr;   // pinned readback of the queue counts
     static constexpr int kRing = 8;
     rt_kernel_args* ring = nullptr;   // pinned host staging slots for async arg uploads
     hipEvent_t ring_ev[kRing] = {};
@@ -69,6 +71,9 @@ struct rt_ctx {
     int n_dnodes = 0;
     bool spec_ok = false;   // every child box lies inside its parent's (speculative walk allowed)
     int shade_k = 32;       // decoupled schedule threshold (env RT_SHADE_K)
+    int debug_flags = 0;    // env RT_DEBUG_FLAGS: ablation runs only (bit 0: Perlin -> 0.5)
+    int wf_slots = 4 << 20; // wavefront: in-flight paths (env RT_WF_SLOTS)
+    int wf_refill = 16;     // wavefront: refill a wave once this many lanes are idle (env RT_WF_REFILL)
     bool uv_always = false;
     bool validated = false;
     uint64_t last_ns = 0;
@@ -349,6 +354,9 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) c->variant = std::atoi(v);
     if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("RT_SHADE_K")) c->shade_k = std::atoi(v);
+    if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
+    if (const char* v = std::getenv("RT_WF_SLOTS")) c->wf_slots = std::max(256, std::atoi(v));
+    if (const char* v = std::getenv("RT_WF_REFILL")) c->wf_refill = std::min(64, std::max(1, std::atoi(v)));
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
         Device& d = c->devs[i];
@@ -375,6 +383,8 @@ int rt_destroy(rt_ctx* c) {
         dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter); dev_free(d.samples);
         dev_free(d.dquads); dev_free(d.dboxes);
+        dev_free(d.wf_q[0]); dev_free(d.wf_q[1]); dev_free(d.wf_hits); dev_free(d.wf_ctr);
+        if (d.wf_host_ctr) (void)hipHostFree(d.wf_host_ctr);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
             if (e) (void)hipEventDestroy(e);
@@ -594,6 +604,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.variant = c->variant;
     a.spec_ok = c->spec_ok ? 1 : 0;
     a.shade_k = c->shade_k;
+    a.debug_flags = c->debug_flags;
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
     a.max_depth = c->max_depth;
@@ -645,6 +656,8 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             chunks_wanted = (int)std::min<long long>(RT_MAX_FRAMES_PER_LAUNCH,
                                                      (c->chunk_target * waves + n_tiles - 1) / n_tiles);
         }
+        const bool wavefront = c->variant == 50;
+        if (wavefront) chunks_wanted = std::max(chunks_wanted, 2);   // always stages per-frame colours
         if (chunks_wanted > 1) {
             size_t per_frame = a.n_pixels * sizeof(float4);
             per_launch = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, c->sample_budget / per_frame));
@@ -655,6 +668,36 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                 d.samples.bytes = need;
             }
         }
+        a.wf_tiles = n_tiles;
+        a.wf_refill = c->wf_refill;
+        if (wavefront) {
+            // in-flight path slots: enough queued rays to keep every lane walking
+            size_t total = (size_t)n_tiles * 64 * (size_t)std::min(per_launch, std::max(n_frames, 1));
+            int slots = (int)std::min<size_t>((size_t)c->wf_slots, std::max<size_t>(total, 1));
+            if (!d.wf_ctr.ptr) {
+                HIPCHK(c, hipMalloc(&d.wf_ctr.ptr, 64));
+                d.wf_ctr.bytes = 64;
+                HIPCHK(c, hipHostMalloc((void**)&d.wf_host_ctr, 64, hipHostMallocDefault));
+            }
+            size_t qb = (size_t)slots * WF_REC_F4 * sizeof(float4), hb = (size_t)slots * WF_HIT_F4 * sizeof(float4);
+            for (int k = 0; k < 2; k++)
+                if (d.wf_q[k].bytes < qb) {
+                    dev_free(d.wf_q[k]);
+                    HIPCHK(c, hipMalloc(&d.wf_q[k].ptr, qb));
+                    d.wf_q[k].bytes = qb;
+                }
+            if (d.wf_hits.bytes < hb) {
+                dev_free(d.wf_hits);
+                HIPCHK(c, hipMalloc(&d.wf_hits.ptr, hb));
+                d.wf_hits.bytes = hb;
+            }
+            a.wf_slots = slots;
+            a.wf_q[0] = (float4*)d.wf_q[0].ptr;
+            a.wf_q[1] = (float4*)d.wf_q[1].ptr;
+            a.wf_hits = (float4*)d.wf_hits.ptr;
+            a.wf_ctr = (unsigned*)d.wf_ctr.ptr;
+            a.wf_next = (unsigned long long*)((char*)d.wf_ctr.ptr + 32);
+        }
         HIPCHK(c, hipEventRecord(d.ev_start, d.stream));
         for (int f0 = 0; f0 < n_frames; f0 += per_launch) {
             int nf = std::min(per_launch, n_frames - f0);
@@ -663,12 +706,13 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             a.n_chunks = std::max(1, std::min(chunks_wanted, nf));
             a.chunk_frames = (nf + a.n_chunks - 1) / a.n_chunks;
             a.n_chunks = (nf + a.chunk_frames - 1) / a.chunk_frames;
-            a.samples = a.n_chunks > 1 ? (float4*)d.samples.ptr : nullptr;
+            a.samples = (a.n_chunks > 1 || wavefront) ? (float4*)d.samples.ptr : nullptr;
+            a.wf_total = (unsigned long long)n_tiles * 64ull * (unsigned long long)nf;
             std::memcpy(a.rand_factors, rand_factors + f0, sizeof(float) * nf);
             int slot = d.ring_pos++ % Device::kRing;
             HIPCHK(c, hipEventSynchronize(d.ring_ev[slot]));   // the copy that last used this slot is done
             d.ring[slot] = a;
-            if (rt_launch_render(d.ring[slot], (rt_kernel_args*)d.args.ptr, d.stream))
+            if (rt_launch_render(d.ring[slot], (rt_kernel_args*)d.args.ptr, d.stream, d.wf_host_ctr))
                 return set_err(c, RT_ERR_DEVICE, std::string("kernel launch failed: ") +
                                                      hipGetErrorString(hipGetLastError()));
             HIPCHK(c, hipEventRecord(d.ring_ev[slot], d.stream));

@@ -25,6 +25,8 @@
 #define RT_NODE_END 0xFFFFu
 #define RT_DFACE_F4 3    // float4 per dquads record
 #define RT_DBOX_F4 18    // float4 per dboxes record
+#define WF_REC_F4 5      // wavefront queue record (path state), float4
+#define WF_HIT_F4 2      // wavefront hit record, float4
 #define RT_LDS_NODE_BYTES (64 * 1024)   // stage the BVH in LDS when it fits (2 workgroups/CU)
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
@@ -77,12 +79,20 @@ struct rt_kernel_args {
     float4* samples;             // chunked mode: per-frame colours [n_frames][n_pixels]; nullptr = direct
     size_t n_pixels;             // local_rows * width
     int shade_k;                 // decoupled schedule: shade once this many lanes wait
+    // wavefront pipeline (variant 50): two path queues, hit records, counters
+    float4* wf_q[2];             // [wf_slots][WF_REC_F4]
+    float4* wf_hits;             // [wf_slots][WF_HIT_F4], by queue position
+    unsigned* wf_ctr;            // [0],[1] queue counts, [2] trace fetch head
+    unsigned long long* wf_next; // next unstarted path id
+    unsigned long long wf_total; // path ids: wf_tiles * 64 * n_frames
+    int wf_slots, wf_tiles, wf_refill;
+    int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int spec_ok;                 // BVH boxes nest (child inside parent): speculative walk allowed
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
 };
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves the default launch shape keeps resident on the current device
-int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream);
+int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream, unsigned* host_ctr);
 // debug: evaluate GLSL built-ins on device (tests)
 int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream);

@@ -346,7 +346,38 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
             uint32_t meta = 0, prims = 0;
             bool leaf = false;
             unsigned long long t0 = STATS ? clock64() : 0;
-            if (i != RT_NODE_END) {
+            if (i != RT_NODE_END && (WHILE_WHILE & 4)) {
+                // software-pipelined: both possible successors (i+1 and the skip
+                // link) are fetched while node i is tested
+                const uint32_t last = (uint32_t)P.n_nodes - 1;
+                float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
+                for (;;) {
+                    if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
+                    meta = __float_as_uint(n1.z);
+                    prims = __float_as_uint(n1.w);
+                    const uint32_t skip = meta & 0xFFFFu;
+                    const uint32_t j1 = min(i + 1, last), j2 = (skip == RT_NODE_END) ? 0u : skip;
+                    float4 b0 = nodes[2 * j1], b1 = nodes[2 * j1 + 1];
+                    float4 c0 = nodes[2 * j2], c1 = nodes[2 * j2 + 1];
+                    bool hitn;
+                    if (!wave_exact) {
+                        hitn = aabb_fast(n0, n1, o, inv, tmin, tmax);
+                    } else {
+                        float lo = tmin, hi = tmax;
+                        slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+                        slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+                        slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+                        hitn = !(hi <= lo);
+                    }
+                    bool inner = (meta & 0xF0000u) == 0;
+                    bool down = hitn && inner;
+                    i = down ? i + 1 : skip;
+                    leaf = hitn && !inner;
+                    if (leaf || i == RT_NODE_END) break;
+                    n0 = down ? b0 : c0;
+                    n1 = down ? b1 : c1;
+                }
+            } else if (i != RT_NODE_END) {
                 for (;;) {
                     if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
                     float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
@@ -407,6 +438,17 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
 }
 
 // ---------------------------------------------------------------- textures
+// rt_unorm8 (c / 255.0f, correctly rounded) without the division: one
+// reciprocal-refinement step, q = c*r, q' = fma(fma(-q, 255, c), r, q) with
+// r = RN(1/255).  Equal to c / 255.0f for every byte c (exhaustive check in
+// tests/test_oracle.py::test_unorm8_refinement_is_exact).
+__device__ __forceinline__ float unorm8_fast(uint32_t c) {
+    const float r = 1.0f / 255.0f;
+    float x = (float)c;
+    float q = x * r;
+    return fmaf(fmaf(-q, 255.0f, x), r, q);
+}
+
 __device__ __forceinline__ void texel(const rt_dtex& T, int x, int y, float out[3]) {
     out[0] = out[1] = out[2] = 0.0f;
     if (!T.data || x < 0 || y < 0 || x >= T.w || y >= T.h) return;
@@ -415,9 +457,9 @@ __device__ __forceinline__ void texel(const rt_dtex& T, int x, int y, float out[
         out[0] = reinterpret_cast<const float*>(T.data)[i];
     } else {
         uint32_t c = reinterpret_cast<const uint32_t*>(T.data)[i];
-        out[0] = rt_unorm8(c & 0xFFu);
-        out[1] = rt_unorm8((c >> 8) & 0xFFu);
-        out[2] = rt_unorm8((c >> 16) & 0xFFu);
+        out[0] = unorm8_fast(c & 0xFFu);
+        out[1] = unorm8_fast((c >> 8) & 0xFFu);
+        out[2] = unorm8_fast((c >> 16) & 0xFFu);
     }
 }
 __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
@@ -505,6 +547,7 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_PERLIN) {    // :79-94
+        if (P.debug_flags & 1) return mk3s(0.5f);   // ablation only (RT_DEBUG_FLAGS), never exact
         float scale = ((float)detail_i / 4095.0f) * 100.0f;
         float accum = 0.0f, weight = 1.0f;
         v3 q = p;
@@ -743,7 +786,12 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     if (rnd(rf, px, py) < 0.5f) d = lights_random(P, p, rf, px, py);
     float lpdf = (P.lights_count > 0) ? lights_pdf_value(P, p, d, S.time) : 0.0f;
     float mpdf;
-    if (mid == RT_MAT_LAMBERTIAN) mpdf = g_max(0.0f, g_normalize1(g_dot(d, normal)) / RT_PI);
+    // cosine_pdf_value (pdf.glsl:32-35): max(0, normalize(cos)/PI) with the scalar
+    // normalize = cos/|cos| in {+1, -1, NaN}: 1/PI exactly when 0 < cos < inf, else 0
+    if (mid == RT_MAT_LAMBERTIAN) {
+        float cs = g_dot(d, normal);
+        mpdf = (cs > 0.0f && cs < INFINITY) ? 1.0f / RT_PI : 0.0f;
+    }
     else if (mid == RT_MAT_ISOTROPIC) mpdf = 1.0f / (4.0f * RT_PI);
     else mpdf = 0.0f;
     float pdf = 0.5f * lpdf + 0.5f * mpdf;
@@ -841,14 +889,16 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
 // per frame in registers and the image is read/written once.  Chunked mode:
 // each frame's colour goes to P.samples[f][pixel] and fold_kernel applies the
 // running mean afterwards in frame order (the same operations, so the same bits).
-template <int WW, bool STATS>
+// SMODE: 0 = direct/chunked chosen at run time, 1 = direct only, 2 = chunked
+// only (no running-mean registers live across the frame loop).
+template <int WW, bool STATS, int SMODE = 0>
 __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, int x, int lr, int f0,
                                              int f1, unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
     int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
     const size_t pix = (size_t)lr * P.width + x;
     float4* px = reinterpret_cast<float4*>(P.image) + pix;
-    const bool direct = P.samples == nullptr;
+    const bool direct = SMODE == 1 || (SMODE == 0 && P.samples == nullptr);
     float4 prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (direct) prev = *px;
     const rt_camera_ubo& C = P.cam;
@@ -1107,7 +1157,7 @@ __device__ __forceinline__ void render_pixel_dec(const KP& P, const float4* __re
 // reaches.  A unit is one 8x8 pixel tile x one chunk of the launch's frames
 // (unit = chunk * n_tiles + tile), so a launch over few tiles (a narrow stripe
 // set at N GPUs) still has many more units than resident waves.
-template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0>
+template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0, int SMODE = 0>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
@@ -1146,8 +1196,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             if (LDSN) render_pixel_dec<DECQ, STATS>(P, s_nodes, xc, lc, f0, f1, valid, st);
             else render_pixel_dec<DECQ, STATS>(P, reinterpret_cast<const float4*>(P.nodes), xc, lc, f0, f1, valid, st);
         } else if (x < P.width && lr < P.local_rows) {
-            if (LDSN) render_pixel<WW, STATS>(P, s_nodes, x, lr, f0, f1, st);
-            else render_pixel<WW, STATS>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, f0, f1, st);
+            if (LDSN) render_pixel<WW, STATS, SMODE>(P, s_nodes, x, lr, f0, f1, st);
+            else render_pixel<WW, STATS, SMODE>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, f0, f1, st);
         }
     }
     if (STATS) {
@@ -1180,6 +1230,261 @@ __global__ void __launch_bounds__(256) fold_kernel(const KP* __restrict__ Pp) {
         prev.w = 1.0f;
     }
     *px = prev;
+}
+
+// ===========================================================================
+// Wavefront pipeline (variant 50).  The launch's (pixel, frame) paths flow
+// through two queues of in-flight paths (rt_device.h: WF_REC_F4 float4 per
+// record) and two kernels per bounce:
+//   wf_trace  — persistent; each lane walks one queued ray and, when its walk
+//               ends, writes the hit record and fetches the next queued ray
+//               (dynamic ray fetch), so lanes do not idle behind the wave's
+//               longest walk; lanes with finite 1/dir keep walking past a hit
+//               leaf (queue of WF_Q leaves, exact re-test on dequeue — the
+//               argument is at struct Trace above);
+//   wf_shade  — one thread per queued path: the rest of ray_color's loop body
+//               (compute.glsl:307-340); a continuing path is appended to the
+//               other queue, a finished one writes its colour to
+//               samples[frame][pixel] and claims the next unstarted path.
+// Per path, the same operations in the same order as the megakernel, so the
+// same bits; fold_kernel then applies the running mean in frame order.
+// Path ids enumerate frame-major, 8x8-tile order within a frame.
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    const unsigned lane = __lane_id();
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// path id -> (local pixel index, frame); false for a padding pixel of a ragged tile
+__device__ __forceinline__ bool wf_decode(const KP& P, unsigned long long pid, int& x, int& lr, int& f) {
+    const int tiles_x = (P.width + 7) >> 3;
+    const unsigned long long per_frame = (unsigned long long)P.wf_tiles * 64ull;
+    f = (int)(pid / per_frame);
+    unsigned long long r = pid - (unsigned long long)f * per_frame;
+    int tile = (int)(r >> 6), within = (int)(r & 63);
+    x = (tile % tiles_x) * 8 + (within & 7);
+    lr = (tile / tiles_x) * 8 + (within >> 3);
+    return x < P.width && lr < P.local_rows;
+}
+
+__device__ __forceinline__ void wf_pixel_xy(const KP& P, int x, int lr, float& fx, float& fy) {
+    int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
+    int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
+    fx = (float)x;
+    fy = (float)y;
+}
+
+// queue record: a = (o, time), b = (d, rf), c = (acc, uvs.a), e = (uvs.b, uvs.c, uvs.kind_idx, depth),
+//               g = (x, lr, frame, 0)
+__device__ __forceinline__ void wf_store(float4* __restrict__ rec, const Path& S, int x, int lr, int f) {
+    rec[0] = make_float4(S.o.x, S.o.y, S.o.z, S.time);
+    rec[1] = make_float4(S.d.x, S.d.y, S.d.z, S.rf);
+    rec[2] = make_float4(S.acc.x, S.acc.y, S.acc.z, S.uvs.a);
+    rec[3] = make_float4(S.uvs.b, S.uvs.c, __int_as_float(S.uvs.kind_idx), __int_as_float(S.depth));
+    rec[4] = make_float4(__int_as_float(x), __int_as_float(lr), __int_as_float(f), 0.0f);
+}
+
+template <int Q, int MINW, int BLOCK, bool LDSN>
+__global__ void __launch_bounds__(BLOCK, MINW) wf_trace(const KP* __restrict__ Pp, int in) {
+    const KP& P = *Pp;
+    extern __shared__ float4 s_nodes[];
+    unsigned* ctr = P.wf_ctr;
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[1 - in] = 0u;   // the shade after us appends there
+    if (LDSN) {
+        const float4* g = reinterpret_cast<const float4*>(P.nodes);
+        for (int k = threadIdx.x; k < 2 * P.n_nodes; k += BLOCK) s_nodes[k] = g[k];
+        __syncthreads();
+    }
+    const float4* __restrict__ nodes = LDSN ? s_nodes : reinterpret_cast<const float4*>(P.nodes);
+    const int n = (int)ctr[in];
+    const float4* __restrict__ q = P.wf_q[in];
+    float4* __restrict__ hits = P.wf_hits;
+    const unsigned lane = __lane_id();
+    int e = -1;            // queue entry this lane walks
+    bool drained = false;  // wave-uniform: the queue has no entries left
+    v3 o = mk3s(0.0f), d = mk3s(0.0f);
+    float time = 0.0f, rf = 0.0f, fx = 0.0f, fy = 0.0f;
+    Trace T;
+    T.ni = RT_NODE_END; T.qn = 0; T.q = 0; T.has = false; T.exact = false; T.spec = false; T.tmax = 0.0f;
+    T.a = 0.0f; T.inv = mk3s(0.0f);
+    T.h.t = 0.0f; T.h.type = 0; T.h.idx = 0; T.h.face = 0; T.h.uv_kind_idx = 0; T.h.uv_a = 0.0f; T.h.uv_b = 0.0f;
+    for (;;) {
+        // ---- refill idle lanes from the queue (one atomic per wave)
+        unsigned long long idle = __ballot(e < 0);
+        if (!drained && __popcll(idle) >= P.wf_refill) {
+            int base = 0;
+            const int first = __ffsll((long long)idle) - 1;
+            if ((int)lane == first) base = (int)atomicAdd(&ctr[2], (unsigned)__popcll(idle));
+            base = __shfl(base, first);
+            if (base + __popcll(idle) >= n) drained = true;
+            if (e < 0) {
+                int k = base + __popcll(idle & lanemask_lt());
+                if (k < n) {
+                    e = k;
+                    const float4* r = q + (size_t)k * WF_REC_F4;
+                    float4 ra = r[0], rb = r[1], rg = r[4];
+                    o = f3(ra); time = ra.w;
+                    d = f3(rb); rf = rb.w;
+                    wf_pixel_xy(P, __float_as_int(rg.x), __float_as_int(rg.y), fx, fy);
+                    // trace_through_bvh's prologue (compute.glsl:226-236)
+                    T.h.t = 0.0f; T.h.type = 0; T.h.idx = 0; T.h.face = 0;
+                    T.h.uv_kind_idx = 0; T.h.uv_a = 0.0f; T.h.uv_b = 0.0f;
+                    T.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                    T.a = g_dot(d, d);
+                    T.tmax = RT_INFINITY;
+                    T.has = false;
+                    T.q = 0;
+                    T.qn = 0;
+                    bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);   // Q1 corner: no hit, no rand()
+                    T.ni = (dir_zero || P.n_nodes == 0) ? RT_NODE_END : 0u;
+                    T.exact = (T.inv.x == -INFINITY) || (T.inv.y == -INFINITY) || (T.inv.z == -INFINITY);
+                    T.spec = P.spec_ok && fabsf(T.inv.x) < INFINITY && fabsf(T.inv.y) < INFINITY &&
+                             fabsf(T.inv.z) < INFINITY;
+                }
+            }
+        }
+        if (__ballot(e >= 0) == 0) {
+            if (drained) break;
+            continue;   // every lane idle but entries remain: refill next round
+        }
+        // ---- node steps until every walking lane has a leaf queued (or walked out)
+        const bool wave_exact = __ballot(e >= 0 && T.exact) != 0;
+        for (;;) {
+            bool walking = e >= 0 && T.ni != RT_NODE_END;
+            if (__ballot(walking && T.qn == 0) == 0) break;
+            if (walking && (T.qn == 0 || (T.spec && T.qn < Q))) node_step(nodes, T, o, wave_exact);
+        }
+        // ---- one queued leaf per lane, exact re-test, prims in order
+        if (e >= 0 && T.qn > 0) {
+            const uint32_t i = (uint32_t)(T.q & 0xFFFFu);
+            T.q >>= 16;
+            T.qn--;
+            float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
+            bool hitn;
+            if (!T.exact) {
+                hitn = aabb_fast(n0, n1, o, T.inv, 0.001f, T.tmax);
+            } else {
+                float lo = 0.001f, hi = T.tmax;
+                slab(n0.x, n0.y, o.x, T.inv.x, lo, hi);
+                slab(n0.z, n0.w, o.y, T.inv.y, lo, hi);
+                slab(n1.x, n1.y, o.z, T.inv.z, lo, hi);
+                hitn = !(hi <= lo);
+            }
+            if (hitn)
+                leaf_prims<false>(P, __float_as_uint(n1.z), __float_as_uint(n1.w), o, d, T.a, time, 0.001f, T.tmax,
+                                  rf, fx, fy, T.h, T.has, nullptr);
+        }
+        // ---- finished walks: write the hit record, free the lane
+        if (e >= 0 && T.ni == RT_NODE_END && T.qn == 0) {
+            float4* hr = hits + (size_t)e * WF_HIT_F4;
+            hr[0] = make_float4(T.h.t, T.h.uv_a, T.h.uv_b, rf);
+            hr[1] = make_float4(__int_as_float(T.has ? 1 : 0), __int_as_float(T.h.type | (T.h.face << 8)),
+                                __int_as_float(T.h.idx), __int_as_float(T.h.uv_kind_idx));
+            e = -1;
+        }
+    }
+}
+
+// Lanes with `need` start the next unstarted paths (one atomic per wave and
+// round); on return a lane has `push` set when it holds a started path (S and
+// x, lr, f set) that needs a walk.  Called by every active lane of the wave.
+__device__ __forceinline__ bool wf_claim(const KP& P, bool need, Path& S, int& x, int& lr, int& f) {
+    bool push = false;
+    for (;;) {
+        unsigned long long m = __ballot(need);
+        if (m == 0) return push;
+        const int first = __ffsll((long long)m) - 1;
+        unsigned long long base = 0;
+        if ((int)__lane_id() == first) base = atomicAdd(P.wf_next, (unsigned long long)__popcll(m));
+        base = __shfl(base, first);
+        if (need) {
+            unsigned long long pid = base + (unsigned long long)__popcll(m & lanemask_lt());
+            if (pid >= P.wf_total) {
+                need = false;
+            } else if (wf_decode(P, pid, x, lr, f)) {
+                float fx, fy;
+                wf_pixel_xy(P, x, lr, fx, fy);
+                const rt_camera_ubo& C = P.cam;
+                v3 cb = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
+                start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, cb);
+                if (S.depth >= P.max_depth) {   // compute.glsl:304 loop bound: final_color stays 0
+                    P.samples[(size_t)f * P.n_pixels + (size_t)lr * P.width + x] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                } else {
+                    S.depth++;
+                    push = true;
+                    need = false;
+                }
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) wf_shade(const KP* __restrict__ Pp, int in, int gen) {
+    const KP& P = *Pp;
+    unsigned* ctr = P.wf_ctr;
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[2] = 0u;   // the next wf_trace's fetch head
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n = gen ? 0 : (int)ctr[in];
+    if (i >= P.wf_slots || (!gen && i >= n)) return;   // whole waves exit together past the end
+    Path S;
+    int x = 0, lr = 0, f = 0;
+    bool push;
+    if (i < n) {
+        const float4* r = P.wf_q[in] + (size_t)i * WF_REC_F4;
+        const float4* hr = P.wf_hits + (size_t)i * WF_HIT_F4;
+        float4 ra = r[0], rb = r[1], rc = r[2], re = r[3], rg = r[4];
+        float4 ha = hr[0], hb = hr[1];
+        S.o = f3(ra); S.time = ra.w;
+        S.d = f3(rb);
+        S.rf = ha.w;   // rand_factor after the walk's medium draws
+        S.acc = f3(rc);
+        S.uvs.a = rc.w; S.uvs.b = re.x; S.uvs.c = re.y; S.uvs.kind_idx = __float_as_int(re.z);
+        S.depth = __float_as_int(re.w);
+        x = __float_as_int(rg.x); lr = __float_as_int(rg.y); f = __float_as_int(rg.z);
+        Hit h;
+        h.t = ha.x; h.uv_a = ha.y; h.uv_b = ha.z;
+        const bool has = __float_as_int(hb.x) != 0;
+        const int tf = __float_as_int(hb.y);
+        h.type = tf & 0xFF; h.face = tf >> 8;
+        h.idx = __float_as_int(hb.z);
+        h.uv_kind_idx = __float_as_int(hb.w);
+        float fx, fy;
+        wf_pixel_xy(P, x, lr, fx, fy);
+        // hit_record.uv as left by this walk (compute.glsl:62)
+        if (h.uv_kind_idx != 0) {
+            bool sph = (h.uv_kind_idx >> 16) == 1;
+            v3 up = add3(S.o, scale3(S.d, h.uv_a));
+            S.uvs.kind_idx = h.uv_kind_idx;
+            S.uvs.a = sph ? up.x : h.uv_a;
+            S.uvs.b = sph ? up.y : h.uv_b;
+            S.uvs.c = sph ? up.z : S.uvs.c;
+        }
+        v3 cur;
+        bool done;
+        if (!has) {
+            cur = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
+            done = true;
+        } else {
+            done = shade(P, S, h, fx, fy, cur);
+        }
+        if (!done) {
+            if (S.depth >= P.max_depth) { cur = mk3s(0.0f); done = true; }
+            else S.depth++;
+        }
+        if (done) P.samples[(size_t)f * P.n_pixels + (size_t)lr * P.width + x] = make_float4(cur.x, cur.y, cur.z, 0.0f);
+        push = !done;
+        if (__ballot(done) != 0) push = wf_claim(P, done, S, x, lr, f) || push;
+    } else {
+        push = wf_claim(P, true, S, x, lr, f);   // initial fill
+    }
+    // append to the other queue: one atomic per wave, contiguous records
+    unsigned long long m = __ballot(push);
+    if (m == 0) return;
+    const int first = __ffsll((long long)m) - 1;
+    int base = 0;
+    if ((int)__lane_id() == first) base = (int)atomicAdd(&ctr[1 - in], (unsigned)__popcll(m));
+    base = __shfl(base, first);
+    if (push) wf_store(P.wf_q[1 - in] + (size_t)(base + __popcll(m & lanemask_lt())) * WF_REC_F4, S, x, lr, f);
 }
 
 __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const float* __restrict__ y,
@@ -1220,7 +1525,50 @@ int rt_resident_waves(void) {
     return cus * 2 * (512 / 64);   // default shape: 2 workgroups of 512 per CU
 }
 
-int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
+// The wavefront pipeline's host loop: fill, then batches of (trace, shade)
+// until the path queue is empty (one small readback per batch), then the fold.
+template <typename K>
+int wf_grid(K kernel, int block, size_t lds) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    return cus * per_cu;
+}
+
+int launch_wavefront(const rt_kernel_args& a, const rt_kernel_args* d, hipStream_t st, unsigned* host_ctr) {
+    constexpr int WB = 512, WM = 4, WQ = 2;
+    size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
+    const bool fits = lds <= RT_LDS_NODE_BYTES;
+    auto trace_k = fits ? wf_trace<WQ, WM, WB, true> : wf_trace<WQ, WM, WB, false>;
+    if (!fits) lds = 0;
+    const int grid = wf_grid(trace_k, WB, lds);
+    if (grid < 0) return -1;
+    const unsigned shade_blocks = (unsigned)((a.wf_slots + 255) / 256);
+    if (hipMemsetAsync(a.wf_ctr, 0, 4 * sizeof(unsigned), st) != hipSuccess) return -1;
+    if (hipMemsetAsync(a.wf_next, 0, sizeof(unsigned long long), st) != hipSuccess) return -1;
+    hipLaunchKernelGGL(wf_shade, dim3(shade_blocks), dim3(256), 0, st, d, 1, 1);   // fill queue 0
+    int in = 0;
+    for (int batch = 0;; batch++) {
+        const int B = batch == 0 ? 8 : 4;
+        for (int k = 0; k < B; k++) {
+            hipLaunchKernelGGL(trace_k, dim3(grid), dim3(WB), lds, st, d, in);
+            hipLaunchKernelGGL(wf_shade, dim3(shade_blocks), dim3(256), 0, st, d, in, 0);
+            in ^= 1;
+        }
+        if (hipMemcpyAsync(host_ctr, a.wf_ctr, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st) != hipSuccess)
+            return -1;
+        if (hipStreamSynchronize(st) != hipSuccess) return -1;
+        if (host_ctr[in] == 0) break;
+        if (batch > 20000) return -1;   // a path ends within max_depth bounces: never reached
+    }
+    unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);
+    hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), 0, st, d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream, unsigned* host_ctr) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.
@@ -1230,9 +1578,14 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
     const rt_kernel_args* d = (const rt_kernel_args*)dargs;
     // Variants (A/B only; all bit-identical):
-    //   0 = 30: while-while, fast slab, branch-free node step, 512 threads / 4 waves per SIMD
+    //   0: variant 30 specialised for direct or chunked launches (SMODE)
+    //   30: while-while, fast slab, branch-free node step, 512 threads / 4 waves per SIMD
     //   31 stats of 30;  10 while-while (exact slab) 512/4w;  19 stats of 10
     //   12 = 30 with global-memory nodes;  15 = 30 at 768 threads / 3 waves
+    if (a.variant == 50) {
+        if (!a.samples || !a.wf_q[0] || !host_ctr) return -1;
+        return launch_wavefront(a, d, st, host_ctr);
+    }
     if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
     size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
     bool fits = lds <= RT_LDS_NODE_BYTES;
@@ -1255,8 +1608,22 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
                            : launch_persistent(render_persistent<3, 4, true, false, 512, 2>, 512, 0, d, st); break;
         case 31: rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512>, 512, lds, d, st)
                            : launch_persistent(render_persistent<3, 4, true, false, 512>, 512, 0, d, st); break;
-        default: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
+        case 32: rc = fits ? launch_persistent(render_persistent<7, 4, false, true, 512, 0, 0>, 512, lds, d, st)
+                           : launch_persistent(render_persistent<7, 4, false, false, 512, 0, 0>, 512, 0, d, st); break;
+        case 33: rc = fits ? launch_persistent(render_persistent<3, 5, false, true, 640, 0, 0>, 640, lds, d, st)
+                           : launch_persistent(render_persistent<3, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
+        case 34: rc = fits ? launch_persistent(render_persistent<7, 5, false, true, 640, 0, 0>, 640, lds, d, st)
+                           : launch_persistent(render_persistent<7, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
+        case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
                            : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
+        default:   // 0: variant 30 specialised for the launch's work split
+            if (a.samples)
+                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2>, 512, lds, d, st)
+                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2>, 512, 0, d, st);
+            else
+                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1>, 512, lds, d, st)
+                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1>, 512, 0, d, st);
+            break;
     }
     if (rc) return rc;
     if (a.samples) {

@@ -178,6 +178,64 @@ def schedule_s(lanes, K, Q, stop="all"):
     return np.array([ni, nl, li, ll, si, sl], float)
 
 
+def schedule_fetch(pool, R, Q=1, lanes_n=64):
+    """Trace-only wavefront schedule with dynamic ray fetch: every trace in
+    `pool` (list of traces, each a list of leaf-hit flags per node) is walked by
+    one lane; lanes whose trace ended are refilled from the pool once >= R lanes
+    are idle (or when the wave would otherwise stall).  While-while walk with a
+    leaf queue of depth Q (Q=1: no speculation).  Returns node/leaf iteration
+    and lane counts."""
+    it = iter(pool)
+    cur = [None] * lanes_n
+    ptr = [0] * lanes_n
+    q = [0] * lanes_n
+    ni = nl = li = ll = 0
+    exhausted = False
+
+    def refill():
+        nonlocal exhausted
+        for k in range(lanes_n):
+            if cur[k] is None and not exhausted:
+                t = next(it, None)
+                if t is None:
+                    exhausted = True
+                else:
+                    cur[k] = t
+                    ptr[k] = 0
+                    q[k] = 0
+    refill()
+    while any(c is not None for c in cur):
+        # node steps
+        while True:
+            walking = [c is not None and ptr[k] < len(c) for k, c in enumerate(cur)]
+            need = [walking[k] and q[k] == 0 for k in range(lanes_n)]
+            if not any(need):
+                break
+            act = [walking[k] and q[k] < Q for k in range(lanes_n)]
+            ni += 1
+            nl += sum(act)
+            for k in range(lanes_n):
+                if act[k]:
+                    if cur[k][ptr[k]]:
+                        q[k] += 1
+                    ptr[k] += 1
+        pend = [q[k] > 0 for k in range(lanes_n)]
+        if any(pend):
+            li += 1
+            ll += sum(pend)
+            for k in range(lanes_n):
+                if pend[k]:
+                    q[k] -= 1
+        for k in range(lanes_n):
+            if cur[k] is not None and ptr[k] >= len(cur[k]) and q[k] == 0:
+                cur[k] = None
+        idle = sum(c is None for c in cur)
+        busy = lanes_n - idle
+        if idle >= R or busy == 0:
+            refill()
+    return np.array([ni, nl, li, ll], float)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", type=int, default=8)
@@ -197,7 +255,9 @@ def main():
     Ks = [int(k) for k in a.K.split(",")]
     A = np.zeros(6)
     B = {k: np.zeros(6) for k in Ks}
-    SQ = [(k, qd, st) for k in (64, 32, 16) for qd in (1, 2, 3, 4) for st in ("all", "full")]
+    SQ = [(k, qd, st) for k in (64, 32) for qd in (1, 2, 3) for st in ("all",)]
+    FR = [(r, qd) for r in (1, 8, 16, 32) for qd in (1, 2, 3)]
+    pool = []
     S = {c: np.zeros(6) for c in SQ}
     for _ in range(a.tiles):
         tx, ty = int(rng.integers(0, W // 8)), int(rng.integers(0, H // 8))
@@ -212,6 +272,8 @@ def main():
             B[k] += schedule_b(lanes, k)
         for c in SQ:
             S[c] += schedule_s(lanes, *c)
+        for lt in lanes:
+            pool.extend(lt)
     ni, nl, li, ll, si, sl = A
     # calibrate per-iteration costs on A: node 48 %, leaf 35 %, shade 12.6 % of cycles
     cn = 0.419 / ni
@@ -227,6 +289,14 @@ def main():
         print(f"B K={k:2d}: node it {ni2:.0f} util {nl2 / ni2 / 64:.2f} | leaf it {li2:.0f} util {ll2 / li2 / 64:.2f} | "
               f"shade it {si2:.0f} util {sl2 / si2 / 64:.2f} | predicted time {cost / base:.3f} x A")
 
+    rng2 = np.random.default_rng(1)
+    order = rng2.permutation(len(pool))
+    pool = [pool[k] for k in order]
+    for r, qd in FR:
+        ni2, nl2, li2, ll2 = schedule_fetch(pool, r, qd)
+        cost = ni2 * cn + li2 * cl + si * cs   # shading at schedule A's count (a separate shade pass)
+        print(f"F R={r:2d} Q={qd}: node it {ni2:.0f} util {nl2 / ni2 / 64:.2f} | leaf it {li2:.0f} util {ll2 / li2 / 64:.2f}"
+              f" | trace cost {(ni2 * cn + li2 * cl) / (ni * cn + li * cl):.3f} x A's trace")
     for c in SQ:
         ni2, nl2, li2, ll2, si2, sl2 = S[c]
         cost = ni2 * cn + li2 * cl + si2 * cs

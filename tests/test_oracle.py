@@ -179,3 +179,38 @@ def test_gallery_scene6():
     assert corr > 0.999, corr
     assert np.abs(d).mean() < 2.0, np.abs(d).mean()
     assert np.abs(d).max() < 10.0, np.abs(d).max()
+
+
+def _rn32(x):
+    """Exact round-to-nearest-even of a Fraction to binary32 (normal range)."""
+    from fractions import Fraction
+    if x == 0:
+        return 0.0
+    sign = -1 if x < 0 else 1
+    x = abs(x)
+    e = x.numerator.bit_length() - x.denominator.bit_length()
+    while Fraction(2) ** e > x:
+        e -= 1
+    while Fraction(2) ** (e + 1) <= x:
+        e += 1
+    scaled = x / Fraction(2) ** (e - 23)          # in [2^23, 2^24)
+    m = scaled.numerator // scaled.denominator
+    rem = scaled - m
+    if rem > Fraction(1, 2) or (rem == Fraction(1, 2) and m % 2 == 1):
+        m += 1
+    return float(sign * m * Fraction(2) ** (e - 23))
+
+
+def test_unorm8_refinement_is_exact():
+    """The kernel's division-free texel conversion (rt_kernel.hip unorm8_fast):
+    q = RN(c*r), q' = fma(fma(-q, 255, c), r, q), r = RN(1/255), equals the
+    reference's c/255 (GL unorm8, rt_glsl.h rt_unorm8) for every byte c."""
+    from fractions import Fraction as F
+    r = F(_rn32(F(1, 255)))
+    for c in range(256):
+        exact = _rn32(F(c, 255))
+        q = F(_rn32(c * r))
+        e = F(_rn32(-q * 255 + c))
+        q2 = _rn32(e * r + q)
+        assert q2 == exact, c
+        assert np.float32(c) / np.float32(255) == np.float32(exact)
