@@ -204,6 +204,12 @@ class RaytraceExecutor:
     def getFinishTime(self):
         return self.finishTime
 
+    def getFinishTimeString(self):               # :76-89
+        ms = self.finishTime
+        hours, minutes, seconds = ms // 3600000, (ms // 60000) % 60, (ms // 1000) % 60
+        s = (f"{hours}hour " if hours > 0 else "") + (f"{minutes}minutes " if minutes > 0 else "")
+        return s + f"{seconds}.{ms % 1000}seconds"
+
     def getLastDispatchTime(self):
         return self.lastDispatchTime
 

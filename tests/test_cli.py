@@ -1,0 +1,116 @@
+"""rtrender — the reference's command line (Main.java:6-70) over the C ABI
+(raytracing-book_amd/host/rt_main.cpp).
+
+CPU: options, defaults and the reference's failure behaviour (commons-cli
+message + help and exit 1; the exceptions Integer.parseInt / Scene throw).
+GPU: the PNG it writes is Texture.saveAsPNG (Texture.java:89-120) of the
+oracle's image, byte for byte, also with rows striped over device slots.
+"""
+import os
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+import rtamd
+from helpers import oracle_image
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(REPO, "raytracing-book_amd", "bin", "rtrender")
+
+
+def run(*args, timeout=120):
+    return subprocess.run([BIN, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+
+
+def read_png(path):
+    """Reader for the writer's output: 8-bit RGB, filter type 0 on every row."""
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, w, h = 8, b"", 0, 0
+    while pos < len(data):
+        n, typ = struct.unpack(">I4s", data[pos:pos + 8])
+        body = data[pos + 8:pos + 8 + n]
+        (crc,) = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])
+        assert crc == zlib.crc32(typ + body) & 0xFFFFFFFF
+        if typ == b"IHDR":
+            w, h, depth, ctype = struct.unpack(">IIBB", body[:10])
+            assert (depth, ctype) == (8, 2)
+        elif typ == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + 3 * w)
+    assert (raw[:, 0] == 0).all()
+    return raw[:, 1:].reshape(h, w, 3)
+
+
+def test_help_lists_the_reference_options():
+    r = run("-h")
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0] == "usage: OpenGL Ray Tracer"
+    for opt, desc in [("-h,--help", "print help message"), ("-s,--scene <arg>", "scene ID"),
+                      ("-r,--resolution <arg>", "screen resolution"),
+                      ("-spp,--sample-per-pixel <arg>", "sample per pixel"), ("-md,--max-depth <arg>", "max depth"),
+                      ("-o,--output <arg>", "output file (must be a .png file)")]:
+        assert any(ln.split()[0] == opt.split()[0] and ln.rstrip().endswith(desc) for ln in lines[1:]), opt
+    assert run("--help").stdout == r.stdout
+
+
+@pytest.mark.parametrize("args,first", [
+    (["-x"], "Unrecognized option: -x"),
+    (["--bogus"], "Unrecognized option: --bogus"),
+    (["-s"], "Missing argument for option: s"),
+    (["--scene"], "Missing argument for option: s"),
+    (["-r", "64:36", "-o"], "Missing argument for option: o"),
+])
+def test_parse_errors_print_the_message_and_help(args, first):
+    r = run(*args)
+    assert r.returncode == 1
+    assert r.stdout.splitlines()[0] == first
+    assert "usage: OpenGL Ray Tracer" in r.stdout
+
+
+@pytest.mark.parametrize("args,err", [
+    (["-s", "abc"], 'java.lang.NumberFormatException: For input string: "abc"'),
+    (["-spp", "1.5"], 'java.lang.NumberFormatException: For input string: "1.5"'),
+    (["-r", "640x480"], 'java.lang.NumberFormatException: For input string: "640x480"'),
+    (["-r", "640"], "java.lang.ArrayIndexOutOfBoundsException"),
+    (["-s", "11"], "java.lang.IllegalArgumentException: Invalid scene ID: 11"),
+    (["--scene=-1"], "java.lang.IllegalArgumentException: Invalid scene ID: -1"),
+])
+def test_bad_values_fail_like_the_reference(args, err):
+    r = run(*args)
+    assert r.returncode == 1
+    assert err in r.stderr
+
+
+@pytest.mark.skipif(rtamd.amd().rt_debug_device_count() > 0, reason="a HIP device is visible")
+def test_render_without_a_device_fails_loudly():
+    r = run("-s6", "-r", "8:8", "-spp", "1")
+    assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sid,devices,per_launch", [(6, "0", 64), (8, "0,0", 4), (0, "0", 2)])
+def test_png_is_saveAsPNG_of_the_oracle_image(gpu, tmp_path, sid, devices, per_launch):
+    w, h, spp = 40, 24, 6
+    out = tmp_path / "out.png"
+    r = run("-s", sid, "-r", f"{w}:{h}", "-spp", spp, "-md", 5, "-o", out, "--devices", devices,
+            "--frames-per-launch", per_launch)
+    assert r.returncode == 0, r.stderr
+    assert "All samples have completed in " in r.stdout
+    assert f"A PNG file has been saved to: {os.path.realpath(out)}" in r.stdout
+    ref = oracle_image(rtamd.Scene(sid, w, h, seed=1), spp, max_depth=5, spp=spp)
+    assert np.array_equal(read_png(out), rtamd.tonemap_rgb8(ref))
+
+
+@pytest.mark.parametrize("ms,text", [(3723456, "1hour 2minutes 3.456seconds"), (59999, "59.999seconds"),
+                                     (61005, "1minutes 1.5seconds"), (0, "0.0seconds")])
+def test_finish_time_string(ms, text):
+    """RaytraceExecutor.getFinishTimeString (RaytraceExecutor.java:76-89), millis unpadded as in Java."""
+    ex = rtamd.RaytraceExecutor(ctx=None)
+    ex.finishTime = ms
+    assert ex.getFinishTimeString() == text
