@@ -215,7 +215,7 @@ def main():
                     "avg_launch_ms": round(avg_launch_ms, 3), "samples_per_launch": samples_per_launch}
 
     out = {
-        "metric": "Msamples/sec (W×H×spp/s) on Book-2 final scene @1080p",
+        "metric": "Msamples/sec (W×H×spp/s) on Book-2 final scene @1080p, 1/2/4/8 GPUs",
         "value": round(value, 2),
         "unit": "Msamples/s",
         "n_gpus": world,
