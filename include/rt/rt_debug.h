@@ -19,6 +19,16 @@ int rt_debug_eval_builtin(int device, int fn, const float* x, const float* y, fl
  * (32-byte rt_dnode records); out may be NULL to query the count. */
 int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t out_cap, int* n_out);
 
+/* Host-only: the exact near-first walk's tables (RT_KERNEL_VARIANT=60) for a
+ * reference BVH upload plus its quad and box records: 8 octant layouts of
+ * n_per_octant threaded rt_dnode records, one word per solid prim (spheres,
+ * then quads, then boxes: reference rank << 16 | reference leaf node) and the
+ * media slots in visit order (4 ints each: medium, leaf, tracker, flags).
+ * Returns 1 when the walk is usable, 0 when every ray takes the exact walk. */
+int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size_t qbytes, const void* boxes,
+                         size_t bbytes, int n_spheres, void* nodes_out, size_t nodes_cap, int* n_per_octant,
+                         unsigned int* info_out, size_t info_cap, int* slots_out, int* n_slots);
+
 /* Diagnostic build of the render kernel with wave-level region timers and
  * active-lane counters (never used for timed numbers).  enable=1 switches the
  * context to it and zeroes the counters; read returns n <= 64 counters. */

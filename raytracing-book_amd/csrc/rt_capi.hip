@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -41,6 +43,8 @@ struct Device {
     DevBuf counter;          // persistent-kernel work-unit counter
     DevBuf samples;          // chunked launches: per-frame colours
     DevBuf wf_q[2], wf_hits, wf_ctr;   // wavefront pipeline (variant 50)
+    DevBuf fnodes, finfo;    // exact near-first walk tables (variant 60)
+    int fast_gen = -1;       // rt_ctx::fast_gen these copies belong to
     unsigned* wf_host_ctr = nullptr;   // pinned readback of the queue counts
     static constexpr int kRing = 8;
     rt_kernel_args* ring = nullptr;   // pinned host staging slots for async arg uploads
@@ -50,6 +54,17 @@ struct Device {
     bool image_bound = false;
     int rank = 0, world = 1;     // stripe assignment of this device
     int local_rows = 0, padded_rows = 0;
+};
+
+// Tables of the exact near-first walk (build_fast below; rt_kernel.hip trace_fast).
+struct FastTables {
+    bool ok = false;
+    std::vector<rt_dnode> nodes;   // 8 octant layouts x n_per threaded nodes
+    int n_per = 0;
+    std::vector<uint32_t> info;    // per solid prim: reference rank << 16 | reference leaf node
+    int base[8] = {0};             // info offset by model type
+    int fm_n = 0, fm_medium[4] = {0}, fm_leaf[4] = {0}, fm_track[4] = {0}, fm_flags[4] = {0};
+    int fl_n = 0, fl_medium[2] = {0}, fl_rank[2] = {0};
 };
 
 }  // namespace
@@ -69,6 +84,9 @@ struct rt_ctx {
     int width = 0, height = 0;
     int proc_rank = 0, proc_world = 1, stripe_rows = 16;
     int n_dnodes = 0;
+    std::vector<rt_dnode> dnodes;   // host copy of the threaded BVH (fast-walk tables are built from it)
+    FastTables fast;
+    int fast_gen = 0;
     bool spec_ok = false;   // every child box lies inside its parent's (speculative walk allowed)
     int shade_k = 32;       // decoupled schedule threshold (env RT_SHADE_K)
     int debug_flags = 0;    // env RT_DEBUG_FLAGS: ablation runs only (bit 0: Perlin -> 0.5)
@@ -247,6 +265,242 @@ bool boxes_nest(const std::vector<rt_dnode>& dn) {
     return true;
 }
 
+// ---- exact near-first walk (variant 60; rt_kernel.hip trace_fast) -------------
+// Built from the reference's threaded BVH (thread_bvh):
+//  * a SAH tree over the BVH's solid prims (sphere / quad / box), each item
+//    bounded by its REFERENCE LEAF box, so every SAH box contains the leaf
+//    boxes below it (joins are exact min/max); binned SAH, <= 2 prims a leaf;
+//  * that tree laid out 8 times as a threaded pre-order with the near child
+//    first for each ray-direction octant (a negative direction on the split
+//    axis visits the upper child first): the stackless walk, ordered;
+//  * per solid prim its reference rank (2 * leaf ordinal + slot: the order in
+//    which the reference tests prims) and its reference leaf node;
+//  * the media slots in the reference order; a slot with solids ranked before
+//    it gets a tracker k (the closest such solid is its ray_t.max), and meta
+//    bit 24 + k marks the SAH subtrees holding solids ranked before it.
+// Eligibility (ok): every quad / box face is axis-aligned, so plane hits are
+// exact to a few ulps (the kernel's windows rely on it); <= 4 media slots,
+// <= 2 trackers, every index in range.  The caller adds the box nesting and
+// the no-image-texture-on-media conditions.
+struct FastItem {
+    float lo[3], hi[3], c[3];
+    int type, idx, rank;
+};
+struct FastNode {
+    float lo[3], hi[3];
+    int kid[2];
+    int axis, first, count, min_rank;
+};
+
+int fast_build_node(std::vector<FastItem>& it, int b, int e, std::vector<FastNode>& T) {
+    FastNode nd;
+    float clo[3], chi[3];
+    for (int k = 0; k < 3; k++) {
+        nd.lo[k] = clo[k] = INFINITY;
+        nd.hi[k] = chi[k] = -INFINITY;
+    }
+    nd.kid[0] = nd.kid[1] = -1;
+    nd.axis = 0;
+    nd.first = b;
+    nd.count = e - b;
+    nd.min_rank = INT_MAX;
+    for (int i = b; i < e; i++) {
+        for (int k = 0; k < 3; k++) {
+            nd.lo[k] = std::min(nd.lo[k], it[i].lo[k]);
+            nd.hi[k] = std::max(nd.hi[k], it[i].hi[k]);
+            clo[k] = std::min(clo[k], it[i].c[k]);
+            chi[k] = std::max(chi[k], it[i].c[k]);
+        }
+        nd.min_rank = std::min(nd.min_rank, it[i].rank);
+    }
+    const int id = (int)T.size();
+    T.push_back(nd);
+    if (e - b <= 2) return id;
+    constexpr int NB = 16;
+    auto area = [](const float* lo, const float* hi) {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    };
+    auto bin_of = [&](const FastItem& q, int ax) {
+        return std::min(NB - 1, (int)((q.c[ax] - clo[ax]) / (chi[ax] - clo[ax]) * NB));
+    };
+    float best = INFINITY;
+    int bax = -1, bsplit = 0;
+    for (int ax = 0; ax < 3; ax++) {
+        if (!(chi[ax] - clo[ax] > 0.0f)) continue;
+        int cnt[NB] = {0};
+        float blo[NB][3], bhi[NB][3];
+        for (int s = 0; s < NB; s++)
+            for (int k = 0; k < 3; k++) {
+                blo[s][k] = INFINITY;
+                bhi[s][k] = -INFINITY;
+            }
+        for (int i = b; i < e; i++) {
+            const int s = bin_of(it[i], ax);
+            cnt[s]++;
+            for (int k = 0; k < 3; k++) {
+                blo[s][k] = std::min(blo[s][k], it[i].lo[k]);
+                bhi[s][k] = std::max(bhi[s][k], it[i].hi[k]);
+            }
+        }
+        float lA[NB], llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int lN[NB], n = 0;
+        for (int s = 0; s < NB; s++) {
+            n += cnt[s];
+            for (int k = 0; k < 3; k++) {
+                llo[k] = std::min(llo[k], blo[s][k]);
+                lhi[k] = std::max(lhi[k], bhi[s][k]);
+            }
+            lN[s] = n;
+            lA[s] = n ? area(llo, lhi) : 0.0f;
+        }
+        float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int rn = 0;
+        for (int s = NB - 1; s >= 1; s--) {   // bins < s left, >= s right
+            rn += cnt[s];
+            for (int k = 0; k < 3; k++) {
+                rlo[k] = std::min(rlo[k], blo[s][k]);
+                rhi[k] = std::max(rhi[k], bhi[s][k]);
+            }
+            const int ln = lN[s - 1];
+            if (ln == 0 || rn == 0) continue;
+            const float cost = lA[s - 1] * ln + area(rlo, rhi) * rn;
+            if (cost < best) {
+                best = cost;
+                bax = ax;
+                bsplit = s;
+            }
+        }
+    }
+    int mid = b;
+    if (bax >= 0) {
+        auto pm = std::partition(it.begin() + b, it.begin() + e,
+                                 [&](const FastItem& q) { return bin_of(q, bax) < bsplit; });
+        mid = (int)(pm - it.begin());
+    }
+    if (mid == b || mid == e) {   // coincident centroids: halve the range along the widest axis
+        int ax = 0;
+        for (int k = 1; k < 3; k++)
+            if (chi[k] - clo[k] > chi[ax] - clo[ax]) ax = k;
+        mid = (b + e) / 2;
+        std::nth_element(it.begin() + b, it.begin() + mid, it.begin() + e,
+                         [ax](const FastItem& x, const FastItem& y) { return x.c[ax] < y.c[ax]; });
+        bax = ax;
+    }
+    const int l = fast_build_node(it, b, mid, T);
+    const int r = fast_build_node(it, mid, e, T);
+    T[id].kid[0] = l;
+    T[id].kid[1] = r;
+    T[id].axis = bax;
+    return id;
+}
+
+void fast_emit(const std::vector<FastNode>& T, const std::vector<FastItem>& it, int n, int oct, const FastTables& F,
+               std::vector<rt_dnode>& out) {
+    const int k = (int)out.size();
+    out.emplace_back();
+    const FastNode& s = T[n];
+    rt_dnode d;
+    d.xmin = s.lo[0]; d.xmax = s.hi[0];
+    d.ymin = s.lo[1]; d.ymax = s.hi[1];
+    d.zmin = s.lo[2]; d.zmax = s.hi[2];
+    uint32_t bits = 0;
+    d.prims = 0;
+    for (int t = 0; t < F.fl_n; t++)
+        if (s.min_rank < F.fl_rank[t]) bits |= 1u << (24 + t);
+    if (s.kid[0] < 0) {
+        for (int j = 0; j < s.count; j++) {
+            const FastItem& q = it[s.first + j];
+            bits |= (uint32_t)q.type << (16 + 4 * j);
+            d.prims |= (uint32_t)q.idx << (16 * j);
+        }
+    } else {
+        const int f = (oct >> s.axis) & 1;
+        fast_emit(T, it, s.kid[f], oct, F, out);
+        fast_emit(T, it, s.kid[1 - f], oct, F, out);
+    }
+    d.meta = bits | (uint32_t)out.size();   // skip = end of this subtree (END patched by the caller)
+    out[k] = d;
+}
+
+FastTables build_fast(const std::vector<rt_dnode>& dn, size_t ns, const rt_quad* quads, size_t nq, const rt_box* boxes,
+                      size_t nb) {
+    FastTables F;
+    auto aligned = [](const rt_quad& q) {
+        return (q.normal[0] == 0.0f) + (q.normal[1] == 0.0f) + (q.normal[2] == 0.0f) == 2;
+    };
+    for (size_t i = 0; i < nq; i++)
+        if (!aligned(quads[i])) return F;
+    for (size_t i = 0; i < nb; i++)
+        for (int f = 0; f < 6; f++)
+            if (!aligned(boxes[i].quads[f])) return F;
+    F.info.assign(ns + nq + nb, 0xFFFFFFFFu);
+    F.base[RT_MODEL_SPHERE] = 0;
+    F.base[RT_MODEL_QUAD] = (int)ns;
+    F.base[RT_MODEL_BOX] = (int)(ns + nq);
+    const size_t count[8] = {0, ns, nq, 0, nb, 0, 0, 0};
+    std::vector<FastItem> items;
+    int rank = 0;
+    bool solid_seen = false;
+    for (int k = 0; k < (int)dn.size(); k++) {
+        const rt_dnode& nd = dn[k];
+        if ((nd.meta & 0xF0000u) == 0) continue;   // inner node
+        int prev = 0;
+        for (int s = 0; s < 2; s++, rank++) {
+            const int ty = (int)((nd.meta >> (16 + 4 * s)) & 0xFu), ix = (int)((nd.prims >> (16 * s)) & 0xFFFFu);
+            const bool solid = ty == RT_MODEL_SPHERE || ty == RT_MODEL_QUAD || ty == RT_MODEL_BOX;
+            if (solid) {
+                if ((size_t)ix >= count[ty] || rank > 0xFFFF) return F;
+                uint32_t& w = F.info[F.base[ty] + ix];
+                if (w == 0xFFFFFFFFu) {   // a prim listed twice keeps its first (earliest) slot
+                    w = ((uint32_t)rank << 16) | (uint32_t)k;
+                    FastItem q;
+                    q.lo[0] = nd.xmin; q.lo[1] = nd.ymin; q.lo[2] = nd.zmin;
+                    q.hi[0] = nd.xmax; q.hi[1] = nd.ymax; q.hi[2] = nd.zmax;
+                    for (int a = 0; a < 3; a++) q.c[a] = 0.5f * (q.lo[a] + q.hi[a]);
+                    q.type = ty;
+                    q.idx = ix;
+                    q.rank = rank;
+                    items.push_back(q);
+                }
+                solid_seen = true;
+            } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
+                if (F.fm_n == 4) return F;
+                int tr = -1;
+                if (solid_seen) {
+                    if (F.fl_n == 2) return F;
+                    tr = F.fl_n++;
+                    F.fl_medium[tr] = ix;
+                    F.fl_rank[tr] = rank;
+                }
+                const int j = F.fm_n++;
+                F.fm_medium[j] = ix;
+                F.fm_leaf[j] = k;
+                F.fm_track[j] = tr;
+                const bool prev_solid = prev == RT_MODEL_SPHERE || prev == RT_MODEL_QUAD || prev == RT_MODEL_BOX;
+                F.fm_flags[j] = (s == 1 && prev == RT_MODEL_CONSTANT_MEDIUM ? 1 : 0) | (s == 1 && prev_solid ? 2 : 0);
+            }
+            prev = ty;
+        }
+    }
+    if (!items.empty()) {
+        std::vector<FastNode> T;
+        T.reserve(2 * items.size());
+        fast_build_node(items, 0, (int)items.size(), T);
+        for (int oct = 0; oct < 8; oct++) {
+            std::vector<rt_dnode> out;
+            fast_emit(T, items, 0, oct, F, out);
+            if (out.size() >= RT_NODE_END) return F;
+            for (rt_dnode& d : out)
+                if ((d.meta & 0xFFFFu) == out.size()) d.meta = (d.meta & ~0xFFFFu) | RT_NODE_END;
+            F.n_per = (int)out.size();
+            F.nodes.insert(F.nodes.end(), out.begin(), out.end());
+        }
+    }
+    F.ok = true;
+    return F;
+}
+
 // Intersection-only record of one quad face (rt_device.h, RT_DFACE_F4): the
 // plane (normal, d) and the 2-D Cramer system of hit_quad (hitting.glsl:90-122)
 // with its axis pair and delta precomputed by the same float expressions.
@@ -310,6 +564,12 @@ int validate(rt_ctx* c) {
                 return set_err(c, RT_ERR_INVALID_ARG, "light references a missing record");
         }
     }
+    // exact near-first walk tables (variant 60): rebuilt after every upload
+    const std::vector<uint8_t>& QB = c->host_buf[RT_BIND_QUADS];
+    const std::vector<uint8_t>& BB = c->host_buf[RT_BIND_BOXES];
+    c->fast = build_fast(c->dnodes, ns, (const rt_quad*)QB.data(), nq, (const rt_box*)BB.data(), nb);
+    c->fast.ok = c->fast.ok && c->spec_ok && !c->uv_always;
+    c->fast_gen++;
     c->validated = true;
     return RT_OK;
 }
@@ -384,6 +644,7 @@ int rt_destroy(rt_ctx* c) {
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter); dev_free(d.samples);
         dev_free(d.dquads); dev_free(d.dboxes);
         dev_free(d.wf_q[0]); dev_free(d.wf_q[1]); dev_free(d.wf_hits); dev_free(d.wf_ctr);
+        dev_free(d.fnodes); dev_free(d.finfo);
         if (d.wf_host_ctr) (void)hipHostFree(d.wf_host_ctr);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
@@ -421,6 +682,7 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
         if (r) return r;
         c->n_dnodes = (int)dn.size();
         c->spec_ok = boxes_nest(dn);
+        c->dnodes = dn;
         dev_bytes.assign((uint8_t*)dn.data(), (uint8_t*)dn.data() + dn.size() * sizeof(rt_dnode));
         src = dev_bytes.data();
         n = dev_bytes.size();
@@ -603,6 +865,18 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.uv_always = c->uv_always;
     a.variant = c->variant;
     a.spec_ok = c->spec_ok ? 1 : 0;
+    const FastTables& F = c->fast;
+    a.fast_ok = F.ok ? 1 : 0;
+    a.n_fnodes = F.n_per;
+    std::memcpy(a.finfo_base, F.base, sizeof(a.finfo_base));
+    a.fm_n = F.fm_n;
+    std::memcpy(a.fm_medium, F.fm_medium, sizeof(a.fm_medium));
+    std::memcpy(a.fm_leaf, F.fm_leaf, sizeof(a.fm_leaf));
+    std::memcpy(a.fm_track, F.fm_track, sizeof(a.fm_track));
+    std::memcpy(a.fm_flags, F.fm_flags, sizeof(a.fm_flags));
+    a.fl_n = F.fl_n;
+    std::memcpy(a.fl_medium, F.fl_medium, sizeof(a.fl_medium));
+    std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
     a.shade_k = c->shade_k;
     a.debug_flags = c->debug_flags;
     a.cam = c->cam;
@@ -644,6 +918,14 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             for (auto& e : d.ring_ev) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         a.tile_counter = (int*)d.counter.ptr;
+        if (d.fast_gen != c->fast_gen) {
+            int rf = dev_alloc_copy(c, d, d.fnodes, F.nodes.data(), F.nodes.size() * sizeof(rt_dnode));
+            if (!rf) rf = dev_alloc_copy(c, d, d.finfo, F.info.data(), F.info.size() * sizeof(uint32_t));
+            if (rf) return rf;
+            d.fast_gen = c->fast_gen;
+        }
+        a.fnodes = (const float4*)d.fnodes.ptr;
+        a.finfo = (const uint32_t*)d.finfo.ptr;
         a.n_pixels = (size_t)d.local_rows * c->width;
         // Frames per launch and the unit split.  Units = tiles x chunks; with too
         // few tiles per resident wave (small images, N-GPU stripes) the frames
@@ -854,6 +1136,38 @@ int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t ou
     return RT_OK;
 }
 
+int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size_t qbytes, const void* boxes,
+                         size_t bbytes, int n_spheres, void* nodes_out, size_t nodes_cap, int* n_per_octant,
+                         uint32_t* info_out, size_t info_cap, int* slots_out, int* n_slots) {
+    if (!bvh || nbytes % sizeof(rt_bvh_node) || qbytes % sizeof(rt_quad) || bbytes % sizeof(rt_box) || n_spheres < 0 ||
+        !n_per_octant || !n_slots || (qbytes && !quads) || (bbytes && !boxes))
+        return RT_ERR_INVALID_ARG;
+    std::vector<rt_dnode> dn;
+    rt_ctx tmp;
+    int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
+    if (r) return r;
+    FastTables F = build_fast(dn, (size_t)n_spheres, (const rt_quad*)quads, qbytes / sizeof(rt_quad),
+                              (const rt_box*)boxes, bbytes / sizeof(rt_box));
+    *n_per_octant = F.n_per;
+    *n_slots = F.fm_n;
+    if (nodes_out) {
+        if (nodes_cap < F.nodes.size() * sizeof(rt_dnode)) return RT_ERR_INVALID_ARG;
+        std::memcpy(nodes_out, F.nodes.data(), F.nodes.size() * sizeof(rt_dnode));
+    }
+    if (info_out) {
+        if (info_cap < F.info.size() * sizeof(uint32_t)) return RT_ERR_INVALID_ARG;
+        std::memcpy(info_out, F.info.data(), F.info.size() * sizeof(uint32_t));
+    }
+    if (slots_out)
+        for (int j = 0; j < F.fm_n; j++) {
+            slots_out[4 * j + 0] = F.fm_medium[j];
+            slots_out[4 * j + 1] = F.fm_leaf[j];
+            slots_out[4 * j + 2] = F.fm_track[j];
+            slots_out[4 * j + 3] = F.fm_flags[j];
+        }
+    return (F.ok && boxes_nest(dn)) ? 1 : 0;
+}
+
 int rt_debug_enable_stats(rt_ctx* c, int on) {
     if (!c) return RT_ERR_INVALID_ARG;
     for (Device& d : c->devs) {
@@ -869,7 +1183,7 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
     // stats twin of the current launch shape: 0/12/15/30 -> 31, 10 -> 19
     if (on) {
         int v = c->variant;
-        c->variant = (v == 10 || v == 19) ? 19 : (v >= 40 && v < 50) ? 49 : 31;
+        c->variant = (v == 10 || v == 19) ? 19 : (v >= 40 && v < 50) ? 49 : (v == 60) ? 60 : 31;
     } else {
         c->variant = 0;
     }

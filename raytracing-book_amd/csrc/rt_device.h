@@ -28,6 +28,8 @@
 #define WF_REC_F4 5      // wavefront queue record (path state), float4
 #define WF_HIT_F4 2      // wavefront hit record, float4
 #define RT_LDS_NODE_BYTES (64 * 1024)   // stage the BVH in LDS when it fits (2 workgroups/CU)
+#define RT_STAT_FAST_TRACES 40          // stats slots (rt_debug_read_stats): traces through the
+#define RT_STAT_FAST_EXACT 41           //   near-first walk, and those that took the exact walk
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
 // continues at index+1 (its RIGHT child, which the reference visits first
@@ -88,6 +90,15 @@ struct rt_kernel_args {
     int wf_slots, wf_tiles, wf_refill;
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int spec_ok;                 // BVH boxes nest (child inside parent): speculative walk allowed
+    // exact near-first walk (variant 60; tables from rt_capi.hip build_fast)
+    const float4* fnodes;        // 8 octant layouts x n_fnodes threaded SAH nodes (rt_dnode), near child first
+    const uint32_t* finfo;       // per solid prim (finfo_base[type] + index): reference rank << 16 | reference leaf
+    int n_fnodes, fast_ok;
+    int finfo_base[8];
+    int fm_n;                    // media slots in the reference's visit order
+    int fm_medium[4], fm_leaf[4], fm_track[4], fm_flags[4];   // flags: 1 same leaf as the previous slot, 2 solid first
+    int fl_n;                    // trackers: the closest solid ranked before a constrained media slot
+    int fl_medium[2], fl_rank[2];
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
 };
 

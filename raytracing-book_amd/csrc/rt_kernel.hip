@@ -188,11 +188,9 @@ __device__ __noinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3
     return false;
 }
 
-// hitting.glsl:162-193 — returns the hit distance t.
-__device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin,
-                                            float tmax, float& rf, float px, float py, float& t) {
-    const rt_medium m = P.media[idx];
-    float t1, t2;
+// hitting.glsl:165-168 — the medium's two boundary hits (no rand() yet).
+__device__ __forceinline__ bool medium_bounds(const KP& P, const rt_medium& m, v3 o, v3 d, float a, float time,
+                                              float& t1, float& t2) {
     if (m.boundary_type == RT_MODEL_SPHERE) {
         // Both boundary hit_sphere calls (:165, :168) see the same ray and sphere:
         // the quadratic and both roots are computed once, then each call's root
@@ -215,20 +213,34 @@ __device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, fl
         if (lo2 < r_lo && r_lo < RT_INFINITY) t2 = r_lo;
         else if (lo2 < r_hi && r_hi < RT_INFINITY) t2 = r_hi;
         else return false;
-    } else {
-        if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, -RT_INFINITY, RT_INFINITY, t1)) return false;
-        if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, t1 + 0.0001f, RT_INFINITY, t2)) return false;
+        return true;
     }
+    if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, -RT_INFINITY, RT_INFINITY, t1)) return false;
+    return boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, t1 + 0.0001f, RT_INFINITY, t2);
+}
+
+// hitting.glsl:169-192 — clamp to ray_t, draw the distance; returns the hit t.
+__device__ __forceinline__ bool medium_tail(float neg_inv_density, float t1, float t2, float a, float tmin, float tmax,
+                                            float& rf, float px, float py, float& t) {
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
     if (t1 < 0.0f) t1 = 0.0f;
     float len = sqrtf(a);   // length(ray.dir); a == dot(dir, dir)
     float inside = (t2 - t1) * len;
-    float hd = m.neg_inv_density * g_log(rnd(rf, px, py));
+    float hd = neg_inv_density * g_log(rnd(rf, px, py));
     if (hd > inside) return false;
     t = t1 + hd / len;
     return true;
+}
+
+// hitting.glsl:162-193 — returns the hit distance t.
+__device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin,
+                                            float tmax, float& rf, float px, float py, float& t) {
+    const rt_medium m = P.media[idx];
+    float t1, t2;
+    if (!medium_bounds(P, m, o, d, a, time, t1, t2)) return false;
+    return medium_tail(m.neg_inv_density, t1, t2, a, tmin, tmax, rf, px, py, t);
 }
 
 // hitting.glsl:55-76 for one axis (branch-free; the same assignments)
@@ -683,6 +695,192 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, float& rf, float 
     return mk3s(0.0f);
 }
 
+// ===========================================================================
+// Exact near-first walk (variant 60).  The reference walks its own median-split
+// BVH in a fixed right-first order (compute.glsl:226-266) and keeps the LAST
+// hit it accepts.  For a ray with a finite origin and finite 1/dir this walk
+// returns the same hit from a SAH tree over the BVH's solid prims, visited
+// near child first (rt_capi.hip build_fast), and replays the media slots in
+// the reference order:
+//  * solids have no side effects, so the reference's hit is the closest one
+//    among the solid prims it VISITS (its acceptance tests are the same
+//    functions), and media draw rand() only in their own slots;
+//  * every SAH box contains the reference leaf boxes of the prims below it
+//    (joins of exactly those boxes) and rounding is monotone, so an SAH node's
+//    slab interval contains theirs: pruning at fprune(best), far above the
+//    error of a hit t against its box entry, skips no leaf whose prim could be
+//    the reference's closest hit;
+//  * the closest solid p is the reference's iff the reference visits p's leaf
+//    L(p).  With no other hit within fwin(best), the reference's ray_t.max at
+//    L(p) exceeds fwin(best); the reference's boxes nest (boxes_nest), so L(p)
+//    passing at fwin(best) means every test on the way to it passes;
+//  * a medium slot sees ray_t.max = min(closest solid ranked before it — the
+//    tracker, checked like p —, earlier medium hits); its leaf test is exact
+//    at that value, or a lower bound of it when only passing matters;
+//  * anything inside the windows (near ties, a medium hit next to the closest
+//    solid, a medium t above ray_t.max, a failed leaf check) returns false and
+//    the caller takes the exact walk with the rand() state restored.
+// Windows: fwin for ties and the acceptance check (2^-14 relative + 1e-4),
+// fprune for pruning (2^-7 relative + 2e-3).  The host enables the walk only
+// when every quad/box face is axis-aligned (plane hits exact to a few ulps),
+// the boxes nest and no medium samples an image texture (uv never goes stale).
+__device__ __forceinline__ float fwin(float t) { return t * (1.0f + 6.103515625e-05f) + 1.0e-4f; }
+__device__ __forceinline__ float fprune(float t) { return t * (1.0f + 7.8125e-03f) + 2.0e-3f; }
+__device__ __forceinline__ bool fnear(float x, float y) { return x <= fwin(y) && y <= fwin(x); }
+__device__ __forceinline__ float fmin2(float x, float y) { return x < y ? x : y; }
+__device__ __forceinline__ float fmax2(float x, float y) { return x > y ? x : y; }
+__device__ __forceinline__ bool ref_leaf_hit(const float4* __restrict__ rn, uint32_t k, v3 o, v3 inv, float tmax) {
+    return aabb_fast(rn[2 * k], rn[2 * k + 1], o, inv, 0.001f, tmax);
+}
+
+__device__ __forceinline__ bool trace_fast(const KP& P, const float4* __restrict__ rn, v3 o, v3 d, float time,
+                                           float& rf, float px, float py, Hit& h, bool& has) {
+    const v3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    if (!(fabsf(inv.x) < INFINITY && fabsf(inv.y) < INFINITY && fabsf(inv.z) < INFINITY && fabsf(o.x) < INFINITY &&
+          fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY))
+        return false;
+    const float a = g_dot(d, d);
+    const float tmin = 0.001f;
+    // trackers: boundary of the constrained slot's medium (its exit bounds the
+    // solids that can be its ray_t.max) and the closest / second closest solid
+    // ranked before the slot
+    float t1_0 = 0.0f, t2_0 = 0.0f, t1_1 = 0.0f, t2_1 = 0.0f;
+    const bool tb0 = P.fl_n > 0 && medium_bounds(P, P.media[P.fl_medium[0]], o, d, a, time, t1_0, t2_0);
+    const bool tb1 = P.fl_n > 1 && medium_bounds(P, P.media[P.fl_medium[1]], o, d, a, time, t1_1, t2_1);
+    float lt0 = RT_INFINITY, lt0b = RT_INFINITY, lt1 = RT_INFINITY, lt1b = RT_INFINITY;
+    uint32_t ll0 = 0u, ll1 = 0u;
+    float pb0 = tb0 ? fprune(t2_0) : -RT_INFINITY;
+    float pb1 = tb1 ? fprune(t2_1) : -RT_INFINITY;
+    const int oct = (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
+    const float4* __restrict__ fn = P.fnodes + (size_t)oct * 2u * (size_t)P.n_fnodes;
+    float best = RT_INFINITY, second = RT_INFINITY, pb = RT_INFINITY;
+    int bty = 0, bix = 0, bface = 0;
+    float bal = 0.0f, bbe = 0.0f;
+    uint32_t i = P.n_fnodes > 0 ? 0u : RT_NODE_END;
+    for (;;) {
+        uint32_t meta = 0, prims = 0;
+        bool leaf = false;
+        while (i != RT_NODE_END) {
+            const float4 n0 = fn[2 * i], n1 = fn[2 * i + 1];
+            meta = __float_as_uint(n1.z);
+            prims = __float_as_uint(n1.w);
+            float bound = pb;
+            if (meta & (1u << 24)) bound = fmax2(bound, pb0);
+            if (meta & (1u << 25)) bound = fmax2(bound, pb1);
+            const bool hitn = aabb_fast(n0, n1, o, inv, tmin, bound);
+            const bool inner = (meta & 0xF0000u) == 0;
+            i = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
+            leaf = hitn && !inner;
+            if (leaf) break;
+        }
+        if (!leaf) break;
+#pragma unroll 1
+        for (int s = 0; s < 2; s++) {
+            const int ty = (int)((meta >> (16 + 4 * s)) & 0xFu);
+            const int ix = (int)((prims >> (16 * s)) & 0xFFFFu);
+            float t = 0.0f, al = 0.0f, be = 0.0f;
+            int face = 0;
+            bool hit = false;
+            if (ty == RT_MODEL_SPHERE)
+                hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, RT_INFINITY, t);
+            else if (ty == RT_MODEL_QUAD)
+                hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, RT_INFINITY, t, al, be);
+            else if (ty == RT_MODEL_BOX)
+                hit = box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, RT_INFINITY, t, face, al, be);
+            if (!hit) continue;
+            if (t < best) {
+                second = best;
+                best = t;
+                bty = ty; bix = ix; bface = face; bal = al; bbe = be;
+                pb = fprune(best);
+            } else if (t < second) {
+                second = t;
+            }
+            if (P.fl_n > 0) {
+                const uint32_t w = P.finfo[P.finfo_base[ty] + ix];
+                const int rank = (int)(w >> 16);
+                if (rank < P.fl_rank[0]) {
+                    if (t < lt0) { lt0b = lt0; lt0 = t; ll0 = w & 0xFFFFu; }
+                    else if (t < lt0b) lt0b = t;
+                    if (tb0) pb0 = fprune(fmin2(lt0, t2_0));
+                }
+                if (P.fl_n > 1 && rank < P.fl_rank[1]) {
+                    if (t < lt1) { lt1b = lt1; lt1 = t; ll1 = w & 0xFFFFu; }
+                    else if (t < lt1b) lt1b = t;
+                    if (tb1) pb1 = fprune(fmin2(lt1, t2_1));
+                }
+            }
+        }
+    }
+    if (best < RT_INFINITY) {
+        if (second <= fwin(best)) return false;
+        if (!ref_leaf_hit(rn, P.finfo[P.finfo_base[bty] + bix] & 0xFFFFu, o, inv, fwin(best))) return false;
+    }
+    // media slots in the reference order
+    float cur = RT_INFINITY;   // ray_t.max after the media hits so far
+    int med = -1, pvis = 2;
+#pragma unroll 1
+    for (int j = 0; j < P.fm_n; j++) {
+        const int mi = P.fm_medium[j], k = P.fm_track[j], flags = P.fm_flags[j];
+        const rt_medium m = P.media[mi];
+        float t1 = 0.0f, t2 = 0.0f;
+        bool bnd;
+        if (k == 0) { bnd = tb0; t1 = t1_0; t2 = t2_0; }
+        else if (k == 1) { bnd = tb1; t1 = t1_1; t2 = t2_1; }
+        else bnd = medium_bounds(P, m, o, d, a, time, t1, t2);
+        float R = RT_INFINITY, Tl = cur;
+        bool exact = k < 0;
+        if (k >= 0 && bnd) {
+            const float l = k ? lt1 : lt0, lb = k ? lt1b : lt0b;
+            if (l < t2) {
+                // the closest solid ranked before the slot is its ray_t.max: one the reference accepts
+                if (lb <= fwin(l) || fnear(cur, l)) return false;
+                if (!ref_leaf_hit(rn, k ? ll1 : ll0, o, inv, fwin(l))) return false;
+                R = l;
+                exact = true;
+            }
+            Tl = fmin2(cur, fmin2(l, t2));   // <= the reference's ray_t.max at the slot's leaf
+        }
+        const float tmax_at = fmin2(cur, R);
+        int vis;   // the slot's leaf is visited: 1 yes, 0 no, 2 unknown
+        if (flags & 1) vis = pvis;
+        else if (!bnd) vis = 2;
+        else if (ref_leaf_hit(rn, (uint32_t)P.fm_leaf[j], o, inv, Tl)) vis = 1;
+        else vis = (exact && !(flags & 2)) ? 0 : 2;
+        pvis = vis;
+        if (!bnd || vis == 0) continue;   // no boundary hit: hit_constant_medium returns before rand()
+        if (vis == 2) return false;
+        float tm;
+        if (!medium_tail(m.neg_inv_density, t1, t2, a, tmin, tmax_at, rf, px, py, tm)) continue;
+        if (!(tm <= tmax_at) || fnear(tm, best)) return false;
+        cur = tm;
+        med = mi;
+    }
+    if (med >= 0 && cur < best) {
+        h.t = cur; h.type = RT_MODEL_CONSTANT_MEDIUM; h.idx = med; h.face = 0;
+        h.uv_kind_idx = 0;
+        has = true;
+    } else if (best < RT_INFINITY) {
+        h.t = best; h.type = bty; h.idx = bix; h.face = bface;
+        h.uv_kind_idx = (bty == RT_MODEL_SPHERE) ? ((1 << 16) | bix) : (2 << 16);
+        h.uv_a = (bty == RT_MODEL_SPHERE) ? best : bal;
+        h.uv_b = bbe;
+        has = true;
+    } else {
+        has = false;
+    }
+    return true;
+}
+
+// Diagnostic counters of the near-first walk (rt_debug_enable_stats).
+__device__ __forceinline__ void fast_count(unsigned long long* g, bool ok) {
+    const unsigned long long all = __ballot(1), fb = __ballot(!ok);
+    if (first_active_lane()) {
+        atomicAdd(g + RT_STAT_FAST_TRACES, (unsigned long long)__popcll(all));
+        atomicAdd(g + RT_STAT_FAST_EXACT, (unsigned long long)__popcll(fb));
+    }
+}
+
 // ------------------------------------------------------------- ray_color
 // Per-lane path state carried between bounces (ray_color's locals).
 struct Path {
@@ -810,7 +1008,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 }
 
 // One iteration of ray_color's loop (compute.glsl:304-340).
-template <int WW, bool STATS>
+template <int WW, bool STATS, bool FAST = false>
 __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, Path& S, float px, float py,
                                        v3& result, unsigned long long* st) {
     if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
@@ -824,7 +1022,22 @@ __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ n
     h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
     // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
     bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
-    bool hit = !dir_zero && trace<WW, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+    bool hit = false;
+    if (dir_zero) {
+    } else if (FAST && P.fast_ok) {
+        const float rf0 = S.rf;
+        bool fh = false;
+        const bool ok = trace_fast(P, nodes, S.o, d, S.time, S.rf, px, py, h, fh);
+        if (P.stats) fast_count(P.stats, ok);
+        if (ok) {
+            hit = fh;
+        } else {   // the exact walk, from the same rand() state
+            S.rf = rf0;
+            hit = trace<WW, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+        }
+    } else {
+        hit = trace<WW, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+    }
     unsigned long long ts = STATS ? clock64() : 0;
     if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
     // hit_record.uv as left by this walk (compute.glsl:62)
@@ -891,7 +1104,7 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
 // running mean afterwards in frame order (the same operations, so the same bits).
 // SMODE: 0 = direct/chunked chosen at run time, 1 = direct only, 2 = chunked
 // only (no running-mean registers live across the frame loop).
-template <int WW, bool STATS, int SMODE = 0>
+template <int WW, bool STATS, int SMODE = 0, bool FAST = false>
 __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, int x, int lr, int f0,
                                              int f1, unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
@@ -918,7 +1131,7 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
             fresh = false;
         }
         v3 cur;
-        if (bounce<WW, STATS>(P, nodes, S, fx, fy, cur, st)) {
+        if (bounce<WW, STATS, FAST>(P, nodes, S, fx, fy, cur, st)) {
             if (direct) {
                 int fc = P.first_frame + f;
                 float n1 = (float)(fc - 1), n = (float)fc;
@@ -1157,7 +1370,7 @@ __device__ __forceinline__ void render_pixel_dec(const KP& P, const float4* __re
 // reaches.  A unit is one 8x8 pixel tile x one chunk of the launch's frames
 // (unit = chunk * n_tiles + tile), so a launch over few tiles (a narrow stripe
 // set at N GPUs) still has many more units than resident waves.
-template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0, int SMODE = 0>
+template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0, int SMODE = 0, bool FAST = false>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
@@ -1196,8 +1409,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             if (LDSN) render_pixel_dec<DECQ, STATS>(P, s_nodes, xc, lc, f0, f1, valid, st);
             else render_pixel_dec<DECQ, STATS>(P, reinterpret_cast<const float4*>(P.nodes), xc, lc, f0, f1, valid, st);
         } else if (x < P.width && lr < P.local_rows) {
-            if (LDSN) render_pixel<WW, STATS, SMODE>(P, s_nodes, x, lr, f0, f1, st);
-            else render_pixel<WW, STATS, SMODE>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, f0, f1, st);
+            if (LDSN) render_pixel<WW, STATS, SMODE, FAST>(P, s_nodes, x, lr, f0, f1, st);
+            else render_pixel<WW, STATS, SMODE, FAST>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, f0, f1, st);
         }
     }
     if (STATS) {
@@ -1616,6 +1829,14 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
                            : launch_persistent(render_persistent<7, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
         case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
                            : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
+        case 60:   // exact near-first walk (trace_fast), otherwise as 0
+            if (a.samples)
+                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2, true>, 512, lds, d, st)
+                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2, true>, 512, 0, d, st);
+            else
+                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1, true>, 512, lds, d, st)
+                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1, true>, 512, 0, d, st);
+            break;
         default:   // 0: variant 30 specialised for the launch's work split
             if (a.samples)
                 rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2>, 512, lds, d, st)
