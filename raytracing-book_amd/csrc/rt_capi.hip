@@ -43,7 +43,8 @@ struct Device {
     DevBuf counter;          // persistent-kernel work-unit counter
     DevBuf samples;          // chunked launches: per-frame colours
     DevBuf wf_q[2], wf_hits, wf_ctr;   // wavefront pipeline (variant 50)
-    DevBuf fnodes, finfo;    // exact near-first walk tables (variant 60)
+    DevBuf fnodes, finfo;    // exact near-first walk tables (variants 60, 61)
+    DevBuf f2inner, f2leaves;
     int fast_gen = -1;       // rt_ctx::fast_gen these copies belong to
     unsigned* wf_host_ctr = nullptr;   // pinned readback of the queue counts
     static constexpr int kRing = 8;
@@ -65,6 +66,12 @@ struct FastTables {
     int base[8] = {0};             // info offset by model type
     int fm_n = 0, fm_medium[4] = {0}, fm_leaf[4] = {0}, fm_track[4] = {0}, fm_flags[4] = {0};
     int fl_n = 0, fl_medium[2] = {0}, fl_rank[2] = {0};
+    // the same tree as two-child nodes for the stack walk (variant 61): per inner node 4 float4 =
+    // left box, right box, (left ref, right ref, tracker bits left | right << 8, 0); a ref >= 0 is an
+    // inner node, ~ref a leaf; a leaf is (meta, prims) as in rt_dnode (types and indices, no skip)
+    std::vector<float4> inner2;
+    std::vector<uint2> leaves2;
+    int depth = 0;   // levels of the tree (the stack walk holds at most depth - 1 entries)
 };
 
 }  // namespace
@@ -423,6 +430,51 @@ void fast_emit(const std::vector<FastNode>& T, const std::vector<FastItem>& it, 
     out[k] = d;
 }
 
+// Two-child layout of tree T (FastTables::inner2 / leaves2).  Returns false when
+// a reference does not fit the 16-bit stack entries.
+int fast_ref(const std::vector<FastNode>& T, const std::vector<FastItem>& it, int n, FastTables& F, int depth);
+bool fast_two_child(const std::vector<FastNode>& T, const std::vector<FastItem>& it, FastTables& F) {
+    F.inner2.clear();
+    F.leaves2.clear();
+    F.depth = 0;
+    fast_ref(T, it, 0, F, 1);
+    return F.inner2.size() / 4 < 32768 && F.leaves2.size() <= 32768;
+}
+int fast_ref(const std::vector<FastNode>& T, const std::vector<FastItem>& it, int n, FastTables& F, int depth) {
+    const FastNode& s = T[n];
+    F.depth = std::max(F.depth, depth);
+    if (s.kid[0] < 0) {
+        uint2 lf = make_uint2(0u, 0u);
+        for (int j = 0; j < s.count; j++) {
+            lf.x |= (uint32_t)it[s.first + j].type << (16 + 4 * j);
+            lf.y |= (uint32_t)it[s.first + j].idx << (16 * j);
+        }
+        F.leaves2.push_back(lf);
+        return ~(int)(F.leaves2.size() - 1);
+    }
+    const int k = (int)(F.inner2.size() / 4);
+    F.inner2.resize(F.inner2.size() + 4);
+    const int rl = fast_ref(T, it, s.kid[0], F, depth + 1);
+    const int rr = fast_ref(T, it, s.kid[1], F, depth + 1);
+    const FastNode& L = T[s.kid[0]];
+    const FastNode& R = T[s.kid[1]];
+    uint32_t bits = 0;
+    for (int t = 0; t < F.fl_n; t++) {
+        if (L.min_rank < F.fl_rank[t]) bits |= 1u << t;
+        if (R.min_rank < F.fl_rank[t]) bits |= 1u << (8 + t);
+    }
+    float4* o = &F.inner2[4 * (size_t)k];
+    o[0] = make_float4(L.lo[0], L.hi[0], L.lo[1], L.hi[1]);
+    o[1] = make_float4(L.lo[2], L.hi[2], R.lo[0], R.hi[0]);
+    o[2] = make_float4(R.lo[1], R.hi[1], R.lo[2], R.hi[2]);
+    float a, b, c;
+    std::memcpy(&a, &rl, 4);
+    std::memcpy(&b, &rr, 4);
+    std::memcpy(&c, &bits, 4);
+    o[3] = make_float4(a, b, c, 0.0f);
+    return k;
+}
+
 FastTables build_fast(const std::vector<rt_dnode>& dn, size_t ns, const rt_quad* quads, size_t nq, const rt_box* boxes,
                       size_t nb) {
     FastTables F;
@@ -496,6 +548,7 @@ FastTables build_fast(const std::vector<rt_dnode>& dn, size_t ns, const rt_quad*
             F.n_per = (int)out.size();
             F.nodes.insert(F.nodes.end(), out.begin(), out.end());
         }
+        if (!fast_two_child(T, items, F)) return F;   // the same tree for the stack walk (variant 61)
     }
     F.ok = true;
     return F;
@@ -644,7 +697,7 @@ int rt_destroy(rt_ctx* c) {
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter); dev_free(d.samples);
         dev_free(d.dquads); dev_free(d.dboxes);
         dev_free(d.wf_q[0]); dev_free(d.wf_q[1]); dev_free(d.wf_hits); dev_free(d.wf_ctr);
-        dev_free(d.fnodes); dev_free(d.finfo);
+        dev_free(d.fnodes); dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves);
         if (d.wf_host_ctr) (void)hipHostFree(d.wf_host_ctr);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
@@ -868,6 +921,9 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_fnodes = F.n_per;
+    a.n_f2inner = (int)(F.inner2.size() / 4);
+    a.n_f2leaves = (int)F.leaves2.size();
+    a.f2depth = F.depth;
     std::memcpy(a.finfo_base, F.base, sizeof(a.finfo_base));
     a.fm_n = F.fm_n;
     std::memcpy(a.fm_medium, F.fm_medium, sizeof(a.fm_medium));
@@ -921,11 +977,15 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         if (d.fast_gen != c->fast_gen) {
             int rf = dev_alloc_copy(c, d, d.fnodes, F.nodes.data(), F.nodes.size() * sizeof(rt_dnode));
             if (!rf) rf = dev_alloc_copy(c, d, d.finfo, F.info.data(), F.info.size() * sizeof(uint32_t));
+            if (!rf) rf = dev_alloc_copy(c, d, d.f2inner, F.inner2.data(), F.inner2.size() * sizeof(float4));
+            if (!rf) rf = dev_alloc_copy(c, d, d.f2leaves, F.leaves2.data(), F.leaves2.size() * sizeof(uint2));
             if (rf) return rf;
             d.fast_gen = c->fast_gen;
         }
         a.fnodes = (const float4*)d.fnodes.ptr;
         a.finfo = (const uint32_t*)d.finfo.ptr;
+        a.f2inner = (const float4*)d.f2inner.ptr;
+        a.f2leaves = (const uint2*)d.f2leaves.ptr;
         a.n_pixels = (size_t)d.local_rows * c->width;
         // Frames per launch and the unit split.  Units = tiles x chunks; with too
         // few tiles per resident wave (small images, N-GPU stripes) the frames
@@ -1183,7 +1243,7 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
     // stats twin of the current launch shape: 0/12/15/30 -> 31, 10 -> 19
     if (on) {
         int v = c->variant;
-        c->variant = (v == 10 || v == 19) ? 19 : (v >= 40 && v < 50) ? 49 : (v == 60) ? 60 : 31;
+        c->variant = (v == 10 || v == 19) ? 19 : (v >= 40 && v < 50) ? 49 : (v == 60 || v == 68) ? 68 : (v == 61 || v == 69) ? 69 : 31;
     } else {
         c->variant = 0;
     }

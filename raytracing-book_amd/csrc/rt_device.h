@@ -28,8 +28,7 @@
 #define WF_REC_F4 5      // wavefront queue record (path state), float4
 #define WF_HIT_F4 2      // wavefront hit record, float4
 #define RT_LDS_NODE_BYTES (64 * 1024)   // stage the BVH in LDS when it fits (2 workgroups/CU)
-#define RT_STAT_FAST_TRACES 40          // stats slots (rt_debug_read_stats): traces through the
-#define RT_STAT_FAST_EXACT 41           //   near-first walk, and those that took the exact walk
+#define RT_LDS_FAST_BYTES (80 * 1024)   // variant 61: two-child tree + stacks in LDS (2 workgroups/CU)
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
 // continues at index+1 (its RIGHT child, which the reference visits first
@@ -99,6 +98,10 @@ struct rt_kernel_args {
     int fm_medium[4], fm_leaf[4], fm_track[4], fm_flags[4];   // flags: 1 same leaf as the previous slot, 2 solid first
     int fl_n;                    // trackers: the closest solid ranked before a constrained media slot
     int fl_medium[2], fl_rank[2];
+    // the same tree as two-child nodes for the stack walk (variant 61; FastTables::inner2/leaves2)
+    const float4* f2inner;       // 4 float4 per inner node: left box, right box, refs + tracker bits
+    const uint2* f2leaves;       // (meta, prims) per leaf
+    int n_f2inner, n_f2leaves, f2depth;
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
 };
 

@@ -38,7 +38,10 @@ __device__ __forceinline__ v3 f3(float4 v) { return mk3(v.x, v.y, v.z); }
 enum {
     ST_TOTAL = 0, ST_START_CYC, ST_START_IT, ST_START_LN, ST_NODE_CYC, ST_NODE_IT, ST_NODE_LN, ST_LEAF_CYC,
     ST_LEAF_IT, ST_LEAF_LN, ST_SPH_LN, ST_QUAD_LN, ST_BOX_LN, ST_MED_LN, ST_SHADE_CYC, ST_SHADE_IT, ST_SHADE_LN,
-    ST_SPH_IT, ST_QUAD_IT, ST_BOX_IT, ST_MED_IT, ST_N
+    ST_SPH_IT, ST_QUAD_IT, ST_BOX_IT, ST_MED_IT,
+    // near-first walk (variants 60/61): traces, those that took the exact walk (and why: 9 reasons),
+    // node steps and prim tests
+    ST_FAST_TRACES, ST_FAST_EXACT, ST_FAST_WHY, ST_FAST_STEPS = ST_FAST_WHY + 9, ST_FAST_TESTS, ST_N
 };
 __device__ __forceinline__ bool first_active_lane() {
     unsigned long long m = __ballot(1);
@@ -698,7 +701,7 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, float& rf, float 
 // ===========================================================================
 // Exact near-first walk (variant 60).  The reference walks its own median-split
 // BVH in a fixed right-first order (compute.glsl:226-266) and keeps the LAST
-// hit it accepts.  For a ray with a finite origin and finite 1/dir this walk
+// hit it accepts.  For a ray with a finite origin and no -inf/NaN in 1/dir this walk
 // returns the same hit from a SAH tree over the BVH's solid prims, visited
 // near child first (rt_capi.hip build_fast), and replays the media slots in
 // the reference order:
@@ -718,8 +721,8 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, float& rf, float 
 //    tracker, checked like p —, earlier medium hits); its leaf test is exact
 //    at that value, or a lower bound of it when only passing matters;
 //  * anything inside the windows (near ties, a medium hit next to the closest
-//    solid, a medium t above ray_t.max, a failed leaf check) returns false and
-//    the caller takes the exact walk with the rand() state restored.
+//    solid, a medium t above ray_t.max, a failed leaf check) returns a nonzero
+//    reason and the caller takes the exact walk with the rand() state restored.
 // Windows: fwin for ties and the acceptance check (2^-14 relative + 1e-4),
 // fprune for pruning (2^-7 relative + 2e-3).  The host enables the walk only
 // when every quad/box face is axis-aligned (plane hits exact to a few ulps),
@@ -729,16 +732,43 @@ __device__ __forceinline__ float fprune(float t) { return t * (1.0f + 7.8125e-03
 __device__ __forceinline__ bool fnear(float x, float y) { return x <= fwin(y) && y <= fwin(x); }
 __device__ __forceinline__ float fmin2(float x, float y) { return x < y ? x : y; }
 __device__ __forceinline__ float fmax2(float x, float y) { return x > y ? x : y; }
+// aabb_fast that also returns the entry distance (near-child-first ordering)
+__device__ __forceinline__ bool aabb_lo(float xmn, float xmx, float ymn, float ymx, float zmn, float zmx, v3 o, v3 inv,
+                                       float tmin, float tmax, float& lo_out) {
+    float t0x = (xmn - o.x) * inv.x, t1x = (xmx - o.x) * inv.x;
+    float t0y = (ymn - o.y) * inv.y, t1y = (ymx - o.y) * inv.y;
+    float t0z = (zmn - o.z) * inv.z, t1z = (zmx - o.z) * inv.z;
+    float lo = v_max(v_max3(tmin, v_min(t0x, t1x), v_min(t0y, t1y)), v_min(t0z, t1z));
+    float hi = v_min(v_min3(tmax, v_max(t0x, t1x), v_max(t0y, t1y)), v_max(t0z, t1z));
+    lo_out = lo;
+    return !(hi <= lo);
+}
+
+// The stack walk's tables and this lane's stack (variant 61): two-child nodes
+// and leaves (LDS when they fit), stack entry e at stack[e * stride].
+#define RT_FAST_STACK 16
+struct FastCtx {
+    const float4* inner;
+    const uint2* leaves;
+    short* stack;
+    int stride;
+};
+
 __device__ __forceinline__ bool ref_leaf_hit(const float4* __restrict__ rn, uint32_t k, v3 o, v3 inv, float tmax) {
     return aabb_fast(rn[2 * k], rn[2 * k + 1], o, inv, 0.001f, tmax);
 }
 
-__device__ __forceinline__ bool trace_fast(const KP& P, const float4* __restrict__ rn, v3 o, v3 d, float time,
-                                           float& rf, float px, float py, Hit& h, bool& has) {
+// MODE 1: threaded octant layouts (global memory); MODE 2: two-child nodes, near
+// child first by entry distance, per-lane stack (fc).
+template <int MODE, bool STATS = false>
+__device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict__ rn, const FastCtx& fc, v3 o, v3 d,
+                                          float time, float& rf, float px, float py, Hit& h, bool& has,
+                                          unsigned long long* st = nullptr) {
     const v3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    if (!(fabsf(inv.x) < INFINITY && fabsf(inv.y) < INFINITY && fabsf(inv.z) < INFINITY && fabsf(o.x) < INFINITY &&
-          fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY))
-        return false;
+    // +inf (a +0 direction component, common: rand() is coarse, so -1 + 2*rand() hits 0) keeps the
+    // fast slab test equal to the reference's and monotone in the box; -inf and NaN do not
+    if (!(inv.x > -INFINITY && inv.y > -INFINITY && inv.z > -INFINITY)) return 1;
+    if (!(fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY)) return 8;
     const float a = g_dot(d, d);
     const float tmin = 0.001f;
     // trackers: boundary of the constrained slot's medium (its exit bounds the
@@ -751,29 +781,13 @@ __device__ __forceinline__ bool trace_fast(const KP& P, const float4* __restrict
     uint32_t ll0 = 0u, ll1 = 0u;
     float pb0 = tb0 ? fprune(t2_0) : -RT_INFINITY;
     float pb1 = tb1 ? fprune(t2_1) : -RT_INFINITY;
-    const int oct = (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
-    const float4* __restrict__ fn = P.fnodes + (size_t)oct * 2u * (size_t)P.n_fnodes;
     float best = RT_INFINITY, second = RT_INFINITY, pb = RT_INFINITY;
     int bty = 0, bix = 0, bface = 0;
     float bal = 0.0f, bbe = 0.0f;
-    uint32_t i = P.n_fnodes > 0 ? 0u : RT_NODE_END;
-    for (;;) {
-        uint32_t meta = 0, prims = 0;
-        bool leaf = false;
-        while (i != RT_NODE_END) {
-            const float4 n0 = fn[2 * i], n1 = fn[2 * i + 1];
-            meta = __float_as_uint(n1.z);
-            prims = __float_as_uint(n1.w);
-            float bound = pb;
-            if (meta & (1u << 24)) bound = fmax2(bound, pb0);
-            if (meta & (1u << 25)) bound = fmax2(bound, pb1);
-            const bool hitn = aabb_fast(n0, n1, o, inv, tmin, bound);
-            const bool inner = (meta & 0xF0000u) == 0;
-            i = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
-            leaf = hitn && !inner;
-            if (leaf) break;
-        }
-        if (!leaf) break;
+    uint32_t n_steps = 0, n_tests = 0;   // diagnostics (P.stats)
+    // the two prims of a leaf: every hit updates the closest / second closest
+    // and the trackers, and tightens the pruning bounds
+    auto leaf_test = [&](uint32_t meta, uint32_t prims) {
 #pragma unroll 1
         for (int s = 0; s < 2; s++) {
             const int ty = (int)((meta >> (16 + 4 * s)) & 0xFu);
@@ -781,6 +795,7 @@ __device__ __forceinline__ bool trace_fast(const KP& P, const float4* __restrict
             float t = 0.0f, al = 0.0f, be = 0.0f;
             int face = 0;
             bool hit = false;
+            n_tests += ty != 0;
             if (ty == RT_MODEL_SPHERE)
                 hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, RT_INFINITY, t);
             else if (ty == RT_MODEL_QUAD)
@@ -811,10 +826,87 @@ __device__ __forceinline__ bool trace_fast(const KP& P, const float4* __restrict
                 }
             }
         }
+    };
+    if (MODE == 1) {
+        const int oct = (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
+        const float4* __restrict__ fn = P.fnodes + (size_t)oct * 2u * (size_t)P.n_fnodes;
+        uint32_t i = P.n_fnodes > 0 ? 0u : RT_NODE_END;
+        for (;;) {
+            uint32_t meta = 0, prims = 0;
+            bool leaf = false;
+            unsigned long long c0 = STATS ? clock64() : 0;
+            while (i != RT_NODE_END) {
+                if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
+                n_steps++;
+                const float4 n0 = fn[2 * i], n1 = fn[2 * i + 1];
+                meta = __float_as_uint(n1.z);
+                prims = __float_as_uint(n1.w);
+                float bound = pb;
+                if (meta & (1u << 24)) bound = fmax2(bound, pb0);
+                if (meta & (1u << 25)) bound = fmax2(bound, pb1);
+                const bool hitn = aabb_fast(n0, n1, o, inv, tmin, bound);
+                const bool inner = (meta & 0xF0000u) == 0;
+                i = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
+                leaf = hitn && !inner;
+                if (leaf) break;
+            }
+            if (STATS) st_add(st, ST_NODE_CYC, clock64() - c0);
+            if (!leaf) break;
+            unsigned long long c1 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+            leaf_test(meta, prims);
+            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - c1);
+        }
+    } else {
+        constexpr int EMPTY = -0x40000000;   // refs are 16-bit: never a node
+        int n = P.n_f2inner > 0 ? 0 : (P.n_f2leaves > 0 ? ~0 : EMPTY);
+        int sp = 0;
+        for (;;) {
+            unsigned long long c0 = STATS ? clock64() : 0;
+            while (n >= 0) {   // inner node: test both children, descend into the nearer
+                if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
+                n_steps++;
+                const float4 A = fc.inner[4 * n], B = fc.inner[4 * n + 1], C = fc.inner[4 * n + 2];
+                const float4 D = fc.inner[4 * n + 3];
+                const int rl = __float_as_int(D.x), rr = __float_as_int(D.y);
+                const uint32_t tb = __float_as_uint(D.z);
+                float bl = pb, br = pb;
+                if (tb & 0x001u) bl = fmax2(bl, pb0);
+                if (tb & 0x002u) bl = fmax2(bl, pb1);
+                if (tb & 0x100u) br = fmax2(br, pb0);
+                if (tb & 0x200u) br = fmax2(br, pb1);
+                float lol = 0.0f, lor = 0.0f;
+                const bool hl = aabb_lo(A.x, A.y, A.z, A.w, B.x, B.y, o, inv, tmin, bl, lol);
+                const bool hr = aabb_lo(B.z, B.w, C.x, C.y, C.z, C.w, o, inv, tmin, br, lor);
+                if (hl && hr) {
+                    if (sp == RT_FAST_STACK) return 9;   // deeper than the stack: the exact walk
+                    const bool lfirst = lol <= lor;
+                    fc.stack[sp * fc.stride] = (short)(lfirst ? rr : rl);
+                    sp++;
+                    n = lfirst ? rl : rr;
+                } else if (hl || hr) {
+                    n = hl ? rl : rr;
+                } else {
+                    n = sp > 0 ? (int)fc.stack[--sp * fc.stride] : EMPTY;
+                }
+            }
+            if (STATS) st_add(st, ST_NODE_CYC, clock64() - c0);
+            if (n == EMPTY) break;
+            unsigned long long c1 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+            const uint2 lf = fc.leaves[~n];
+            leaf_test(lf.x, lf.y);
+            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - c1);
+            n = sp > 0 ? (int)fc.stack[--sp * fc.stride] : EMPTY;
+        }
+    }
+    if (STATS) {
+        atomicAdd(st + ST_FAST_STEPS, (unsigned long long)n_steps);
+        atomicAdd(st + ST_FAST_TESTS, (unsigned long long)n_tests);
     }
     if (best < RT_INFINITY) {
-        if (second <= fwin(best)) return false;
-        if (!ref_leaf_hit(rn, P.finfo[P.finfo_base[bty] + bix] & 0xFFFFu, o, inv, fwin(best))) return false;
+        if (second <= fwin(best)) return 2;
+        if (!ref_leaf_hit(rn, P.finfo[P.finfo_base[bty] + bix] & 0xFFFFu, o, inv, fwin(best))) return 3;
     }
     // media slots in the reference order
     float cur = RT_INFINITY;   // ray_t.max after the media hits so far
@@ -829,30 +921,39 @@ __device__ __forceinline__ bool trace_fast(const KP& P, const float4* __restrict
         else if (k == 1) { bnd = tb1; t1 = t1_1; t2 = t2_1; }
         else bnd = medium_bounds(P, m, o, d, a, time, t1, t2);
         float R = RT_INFINITY, Tl = cur;
-        bool exact = k < 0;
+        bool exact = k < 0;   // Tl is the reference's ray_t.max at the slot's leaf, not just a lower bound
+        bool verified = false;
         if (k >= 0 && bnd) {
             const float l = k ? lt1 : lt0, lb = k ? lt1b : lt0b;
             if (l < t2) {
                 // the closest solid ranked before the slot is its ray_t.max: one the reference accepts
-                if (lb <= fwin(l) || fnear(cur, l)) return false;
-                if (!ref_leaf_hit(rn, k ? ll1 : ll0, o, inv, fwin(l))) return false;
+                if (lb <= fwin(l) || fnear(cur, l)) return 4;
+                if (!ref_leaf_hit(rn, k ? ll1 : ll0, o, inv, fwin(l))) return 5;
                 R = l;
-                exact = true;
+                verified = true;
             }
-            Tl = fmin2(cur, fmin2(l, t2));   // <= the reference's ray_t.max at the slot's leaf
+            // The reference's ray_t.max at the leaf is min(cur, closest accepted solid ranked before
+            // the leaf) >= min(cur, l, t2): an earlier-ranked solid below min(l, t2) would be l.  It
+            // equals Tl when cur is the smaller one, or when l is verified and no solid precedes the
+            // medium inside its own leaf.
+            Tl = fmin2(cur, fmin2(l, t2));
+            exact = (cur <= fmin2(l, t2)) || (verified && !(flags & 2));
         }
         const float tmax_at = fmin2(cur, R);
+        // the clamped interval [max(t1, tmin), min(t2, ray_t.max)] is empty whatever ray_t.max is:
+        // hit_constant_medium returns before rand() whether or not the leaf is visited
+        const bool no_draw = bnd && !((t1 < tmin ? tmin : t1) < t2);
         int vis;   // the slot's leaf is visited: 1 yes, 0 no, 2 unknown
         if (flags & 1) vis = pvis;
         else if (!bnd) vis = 2;
         else if (ref_leaf_hit(rn, (uint32_t)P.fm_leaf[j], o, inv, Tl)) vis = 1;
         else vis = (exact && !(flags & 2)) ? 0 : 2;
         pvis = vis;
-        if (!bnd || vis == 0) continue;   // no boundary hit: hit_constant_medium returns before rand()
-        if (vis == 2) return false;
+        if (!bnd || vis == 0 || no_draw) continue;   // hit_constant_medium returns before rand()
+        if (vis == 2) return 6;
         float tm;
         if (!medium_tail(m.neg_inv_density, t1, t2, a, tmin, tmax_at, rf, px, py, tm)) continue;
-        if (!(tm <= tmax_at) || fnear(tm, best)) return false;
+        if (!(tm <= tmax_at) || fnear(tm, best)) return 7;
         cur = tm;
         med = mi;
     }
@@ -869,16 +970,17 @@ __device__ __forceinline__ bool trace_fast(const KP& P, const float4* __restrict
     } else {
         has = false;
     }
-    return true;
+    return 0;
 }
 
-// Diagnostic counters of the near-first walk (rt_debug_enable_stats).
-__device__ __forceinline__ void fast_count(unsigned long long* g, bool ok) {
-    const unsigned long long all = __ballot(1), fb = __ballot(!ok);
+// Diagnostic counters of the near-first walk (stats builds; st = the wave's LDS counters).
+__device__ __forceinline__ void fast_count(unsigned long long* st, int why) {
+    const unsigned long long all = __ballot(1), fb = __ballot(why != 0);
     if (first_active_lane()) {
-        atomicAdd(g + RT_STAT_FAST_TRACES, (unsigned long long)__popcll(all));
-        atomicAdd(g + RT_STAT_FAST_EXACT, (unsigned long long)__popcll(fb));
+        atomicAdd(st + ST_FAST_TRACES, (unsigned long long)__popcll(all));
+        atomicAdd(st + ST_FAST_EXACT, (unsigned long long)__popcll(fb));
     }
+    if (why) atomicAdd(st + ST_FAST_WHY + why - 1, 1ull);   // reasons 1..9
 }
 
 // ------------------------------------------------------------- ray_color
@@ -1008,9 +1110,9 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 }
 
 // One iteration of ray_color's loop (compute.glsl:304-340).
-template <int WW, bool STATS, bool FAST = false>
-__device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, Path& S, float px, float py,
-                                       v3& result, unsigned long long* st) {
+template <int WW, bool STATS, int FAST = 0>
+__device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, Path& S,
+                                       float px, float py, v3& result, unsigned long long* st) {
     if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
         result = mk3s(0.0f);
         return true;
@@ -1027,9 +1129,9 @@ __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ n
     } else if (FAST && P.fast_ok) {
         const float rf0 = S.rf;
         bool fh = false;
-        const bool ok = trace_fast(P, nodes, S.o, d, S.time, S.rf, px, py, h, fh);
-        if (P.stats) fast_count(P.stats, ok);
-        if (ok) {
+        const int why = trace_fast<FAST, STATS>(P, nodes, fc, S.o, d, S.time, S.rf, px, py, h, fh, st);
+        if (STATS) fast_count(st, why);
+        if (why == 0) {
             hit = fh;
         } else {   // the exact walk, from the same rand() state
             S.rf = rf0;
@@ -1104,9 +1206,9 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
 // running mean afterwards in frame order (the same operations, so the same bits).
 // SMODE: 0 = direct/chunked chosen at run time, 1 = direct only, 2 = chunked
 // only (no running-mean registers live across the frame loop).
-template <int WW, bool STATS, int SMODE = 0, bool FAST = false>
-__device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, int x, int lr, int f0,
-                                             int f1, unsigned long long* st) {
+template <int WW, bool STATS, int SMODE = 0, int FAST = 0>
+__device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, int x,
+                                             int lr, int f0, int f1, unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
     int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
     const size_t pix = (size_t)lr * P.width + x;
@@ -1131,7 +1233,7 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
             fresh = false;
         }
         v3 cur;
-        if (bounce<WW, STATS, FAST>(P, nodes, S, fx, fy, cur, st)) {
+        if (bounce<WW, STATS, FAST>(P, nodes, fc, S, fx, fy, cur, st)) {
             if (direct) {
                 int fc = P.first_frame + f;
                 float n1 = (float)(fc - 1), n = (float)fc;
@@ -1370,7 +1472,7 @@ __device__ __forceinline__ void render_pixel_dec(const KP& P, const float4* __re
 // reaches.  A unit is one 8x8 pixel tile x one chunk of the launch's frames
 // (unit = chunk * n_tiles + tile), so a launch over few tiles (a narrow stripe
 // set at N GPUs) still has many more units than resident waves.
-template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0, int SMODE = 0, bool FAST = false>
+template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0, int SMODE = 0, int FAST = 0>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
@@ -1383,12 +1485,37 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         for (int k = tid; k < (BLOCK / 64) * ST_N; k += BLOCK) (&s_stats[0][0])[k] = 0;
         st = s_stats[tid / 64];
     }
-    if (LDSN) {
+    // FAST 2 keeps its two-child tree + stack in LDS (the reference nodes stay in
+    // global memory: leaf checks and the rare exact walk); otherwise LDSN stages
+    // the reference's threaded nodes
+    FastCtx fc;
+    fc.inner = P.f2inner;
+    fc.leaves = P.f2leaves;
+    fc.stack = nullptr;
+    fc.stride = BLOCK;
+    if (FAST == 2) {
+        const int n4 = 4 * P.n_f2inner, nl4 = (P.n_f2leaves + 1) / 2;
+        if (LDSN) {
+            for (int k = tid; k < n4; k += BLOCK) s_nodes[k] = P.f2inner[k];
+            const float4* gl = reinterpret_cast<const float4*>(P.f2leaves);
+            for (int k = tid; k < P.n_f2leaves / 2; k += BLOCK) s_nodes[n4 + k] = gl[k];
+            if ((P.n_f2leaves & 1) && tid == 0) {
+                const uint2 last = P.f2leaves[P.n_f2leaves - 1];
+                reinterpret_cast<uint2*>(s_nodes + n4)[P.n_f2leaves - 1] = last;
+            }
+            fc.inner = s_nodes;
+            fc.leaves = reinterpret_cast<const uint2*>(s_nodes + n4);
+            fc.stack = reinterpret_cast<short*>(s_nodes + n4 + nl4) + tid;
+        } else {
+            fc.stack = reinterpret_cast<short*>(s_nodes) + tid;
+        }
+    } else if (LDSN) {
         const float4* g = reinterpret_cast<const float4*>(P.nodes);
         for (int k = tid; k < 2 * P.n_nodes; k += BLOCK) s_nodes[k] = g[k];
     }
     if (LDSN || STATS) __syncthreads();
     if (STATS) t_begin = clock64();
+    const float4* __restrict__ rnodes = (LDSN && FAST != 2) ? s_nodes : reinterpret_cast<const float4*>(P.nodes);
     const int tiles_x = (P.width + 7) >> 3;
     const int n_tiles = tiles_x * ((P.local_rows + 7) >> 3);
     const int n_units = n_tiles * P.n_chunks;
@@ -1409,8 +1536,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             if (LDSN) render_pixel_dec<DECQ, STATS>(P, s_nodes, xc, lc, f0, f1, valid, st);
             else render_pixel_dec<DECQ, STATS>(P, reinterpret_cast<const float4*>(P.nodes), xc, lc, f0, f1, valid, st);
         } else if (x < P.width && lr < P.local_rows) {
-            if (LDSN) render_pixel<WW, STATS, SMODE, FAST>(P, s_nodes, x, lr, f0, f1, st);
-            else render_pixel<WW, STATS, SMODE, FAST>(P, reinterpret_cast<const float4*>(P.nodes), x, lr, f0, f1, st);
+            render_pixel<WW, STATS, SMODE, FAST>(P, rnodes, fc, x, lr, f0, f1, st);
         }
     }
     if (STATS) {
@@ -1723,6 +1849,10 @@ int launch_persistent(K kernel, int block, size_t lds, const rt_kernel_args* d, 
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+        return -1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
     hipLaunchKernelGGL(kernel, dim3(cus * per_cu), dim3(block), lds, st, d);
@@ -1830,13 +1960,33 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
         case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
                            : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
         case 60:   // exact near-first walk (trace_fast), otherwise as 0
-            if (a.samples)
-                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2, true>, 512, lds, d, st)
-                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2, true>, 512, 0, d, st);
+        case 68:   // stats twin of 60
+            if (a.variant == 68)
+                rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512, 0, 0, 1>, 512, lds, d, st)
+                          : launch_persistent(render_persistent<3, 4, true, false, 512, 0, 0, 1>, 512, 0, d, st);
+            else if (a.samples)
+                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2, 1>, 512, lds, d, st)
+                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2, 1>, 512, 0, d, st);
             else
-                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1, true>, 512, lds, d, st)
-                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1, true>, 512, 0, d, st);
+                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1, 1>, 512, lds, d, st)
+                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1, 1>, 512, 0, d, st);
             break;
+        case 61:     // exact near-first stack walk over the two-child tree in LDS, otherwise as 0
+        case 69: {   // stats twin of 61
+            const size_t stack_b = (size_t)RT_FAST_STACK * 512 * sizeof(short);
+            const size_t tree_b = (size_t)a.n_f2inner * 64 + (size_t)((a.n_f2leaves + 1) / 2) * 16;
+            const bool in_lds = tree_b + stack_b <= RT_LDS_FAST_BYTES;
+            const size_t l2 = in_lds ? tree_b + stack_b : stack_b;
+            if (a.variant == 69)
+                rc = launch_persistent(render_persistent<3, 4, true, true, 512, 0, 0, 2>, 512, l2, d, st);
+            else if (a.samples)
+                rc = in_lds ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2, 2>, 512, l2, d, st)
+                            : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2, 2>, 512, l2, d, st);
+            else
+                rc = in_lds ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1, 2>, 512, l2, d, st)
+                            : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1, 2>, 512, l2, d, st);
+            break;
+        }
         default:   // 0: variant 30 specialised for the launch's work split
             if (a.samples)
                 rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2>, 512, lds, d, st)

@@ -15,7 +15,7 @@ from helpers import bit_equal, mismatch_report, oracle_image
 
 pytestmark = pytest.mark.gpu
 
-TRACES, EXACT = 40, 41   # rt_device.h RT_STAT_FAST_*
+TRACES, EXACT, WHY, STEPS, TESTS = 21, 22, 23, 32, 33   # rt_kernel.hip ST_FAST_* (stats builds)
 
 
 def render(monkeypatch, variant, scene, frames, depth=5, spp=None, stats=False):
@@ -33,30 +33,35 @@ def render(monkeypatch, variant, scene, frames, depth=5, spp=None, stats=False):
     if stats:
         buf = (ctypes.c_ulonglong * 64)()
         assert L.rt_debug_read_stats(ctx._h, buf, 64) == 0
-        counters = (buf[TRACES], buf[EXACT])
+        counters = (buf[TRACES], buf[EXACT], [buf[WHY + r] for r in range(9)], buf[STEPS], buf[TESTS])
     ctx.close()
     return img, counters
 
 
+@pytest.mark.parametrize("variant", [60, 61])
 @pytest.mark.parametrize("sid", range(10))
-def test_fast_walk_matches_oracle(gpu, monkeypatch, sid):
+def test_fast_walk_matches_oracle(gpu, monkeypatch, sid, variant):
     scene = rtamd.Scene(sid, 64, 36, seed=1)
-    out, _ = render(monkeypatch, 60, scene, 4)
+    out, _ = render(monkeypatch, variant, scene, 4)
     ref = oracle_image(scene, 4)
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
+@pytest.mark.parametrize("variant", [60, 61])
 @pytest.mark.parametrize("sid,frames", [(8, 16), (0, 8), (2, 4), (3, 4), (5, 8), (9, 8)])
-def test_fast_walk_equals_reference_walk_1080p(gpu, monkeypatch, sid, frames):
+def test_fast_walk_equals_reference_walk_1080p(gpu, monkeypatch, sid, frames, variant):
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
-    ref, _ = render(monkeypatch, 0, scene, frames)
-    out, _ = render(monkeypatch, 60, scene, frames)
+    ref, _ = render(monkeypatch, 30, scene, frames)
+    out, _ = render(monkeypatch, variant, scene, frames)
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
-@pytest.mark.parametrize("sid,max_exact", [(8, 0.02), (0, 0.02)])
-def test_fast_walk_is_taken(gpu, monkeypatch, sid, max_exact):
+@pytest.mark.parametrize("variant", [60, 61])
+@pytest.mark.parametrize("sid,max_exact", [(8, 0.002), (0, 0.002)])
+def test_fast_walk_is_taken(gpu, monkeypatch, sid, max_exact, variant):
     scene = rtamd.Scene(sid, 640, 360, seed=1)
-    _, (traces, exact) = render(monkeypatch, 60, scene, 4, stats=True)
-    print(f"scene {sid}: {traces} traces, {exact} took the exact walk ({exact / max(traces, 1):.5f})")
+    _, (traces, exact, why, steps, tests) = render(monkeypatch, variant, scene, 4, stats=True)
+    print(f"variant {variant} scene {sid}: {traces} traces, {exact} took the exact walk ({exact / max(traces, 1):.5f}); "
+          f"reasons 1-9 (1/dir inf, tie, leaf, tracker tie, tracker leaf, medium leaf, medium t, origin, stack): {why}; "
+          f"{steps / max(traces, 1):.1f} node steps, {tests / max(traces, 1):.2f} prim tests per trace")
     assert traces > 640 * 360 * 4 and exact < max_exact * traces
