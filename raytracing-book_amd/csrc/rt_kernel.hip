@@ -150,28 +150,33 @@ __device__ __forceinline__ bool quad_test(const float4* __restrict__ f, v3 o, v3
 // the interior test — the same tests on the same values, so the same result.
 __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3 d, float tmin, float tmax, float& t,
                                          int& face, float& alpha, float& beta) {
-    float ti[6];
-    unsigned cand = 0;
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        float4 pl = fb[i];
-        v3 n = f3(pl);
-        float denom = g_dot(n, d);
-        ti[i] = (pl.w - g_dot(n, o)) / denom;   // unused when |denom| < 1e-8
-        if (!(fabsf(denom) < 1e-8f) && (tmin <= ti[i] && ti[i] <= tmax)) cand |= 1u << i;
-    }
     bool has = false;
+    // two halves of three faces: fewer live registers than six at once
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-        if ((cand >> i) & 1u) {
-            float al, be;
-            if (ti[i] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[i], al, be)) {
-                tmax = ti[i];
-                t = ti[i];
-                face = i;
-                alpha = al;
-                beta = be;
-                has = true;
+    for (int h = 0; h < 6; h += 3) {
+        float ti[3];
+        unsigned cand = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            float4 pl = fb[h + k];
+            v3 n = f3(pl);
+            float denom = g_dot(n, d);
+            ti[k] = (pl.w - g_dot(n, o)) / denom;   // unused when |denom| < 1e-8
+            if (!(fabsf(denom) < 1e-8f) && (tmin <= ti[k] && ti[k] <= tmax)) cand |= 1u << k;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int i = h + k;
+            if ((cand >> k) & 1u) {
+                float al, be;
+                if (ti[k] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[k], al, be)) {
+                    tmax = ti[k];
+                    t = ti[k];
+                    face = i;
+                    alpha = al;
+                    beta = be;
+                    has = true;
+                }
             }
         }
     }
