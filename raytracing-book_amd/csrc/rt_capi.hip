@@ -935,6 +935,14 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
     a.shade_k = c->shade_k;
     a.debug_flags = c->debug_flags;
+    // Perlin table in LDS after the nodes (default launch shapes only; rt_kernel.hip texture_color)
+    a.perlin_slot = a.perlin_lds = -1;
+    for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
+        if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
+    if (a.perlin_slot >= 0 && (c->variant == 0 || c->variant == 30) &&
+        (size_t)c->n_dnodes * sizeof(rt_dnode) + (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] * 4 <=
+            RT_LDS_NODE_BYTES)
+        a.perlin_lds = 2 * c->n_dnodes;
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
     a.max_depth = c->max_depth;

@@ -88,6 +88,8 @@ struct rt_kernel_args {
     unsigned long long wf_total; // path ids: wf_tiles * 64 * n_frames
     int wf_slots, wf_tiles, wf_refill;
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
+    int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1
+    int perlin_lds;              // its float4 offset in the dynamic LDS (after the nodes), or -1
     int spec_ok;                 // BVH boxes nest (child inside parent): speculative walk allowed
     // exact near-first walk (variant 60; tables from rt_capi.hip build_fast)
     const float4* fnodes;        // 8 octant layouts x n_fnodes threaded SAH nodes (rt_dnode), near child first

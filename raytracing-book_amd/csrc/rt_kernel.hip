@@ -488,8 +488,17 @@ __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
     return t[0];
 }
 
+// The kernels' dynamic LDS (render_persistent stages the BVH there, and the
+// Perlin table after it when P.perlin_lds >= 0).
+extern __shared__ float4 rt_dyn_lds[];
+
+// texel_r of an R32F table given as a plain pointer (LDS copy or global)
+__device__ __forceinline__ float table_r(const float* tab, int w, int h, int x, int y) {
+    return (!tab || x < 0 || y < 0 || x >= w || y >= h) ? 0.0f : tab[y * w + x];
+}
+
 // texture.glsl:38-77 with perlin_interp (19-36) fused; Hermite applied twice (Q6)
-__device__ __forceinline__ float perlin_noise(const rt_dtex& T, v3 p) {
+__device__ __forceinline__ float perlin_noise(const float* tab, int tw, int th, v3 p) {
     float u = p.x - floorf(p.x);
     float v = p.y - floorf(p.y);
     float w = p.z - floorf(p.z);
@@ -505,15 +514,15 @@ __device__ __forceinline__ float perlin_noise(const rt_dtex& T, v3 p) {
     float accum = 0.0f;
 #pragma unroll
     for (int di = 0; di < 2; di++) {
-        int px = rt_f2i(texel_r(T, 3, (i + di) & 255));
+        int px = rt_f2i(table_r(tab, tw, th, 3, (i + di) & 255));
 #pragma unroll
         for (int dj = 0; dj < 2; dj++) {
-            int py = rt_f2i(texel_r(T, 4, (j + dj) & 255));
+            int py = rt_f2i(table_r(tab, tw, th, 4, (j + dj) & 255));
 #pragma unroll
             for (int dk = 0; dk < 2; dk++) {
-                int pz = rt_f2i(texel_r(T, 5, (k + dk) & 255));
+                int pz = rt_f2i(table_r(tab, tw, th, 5, (k + dk) & 255));
                 int idx = px ^ py ^ pz;
-                v3 c = mk3(texel_r(T, 0, idx), texel_r(T, 1, idx), texel_r(T, 2, idx));
+                v3 c = mk3(table_r(tab, tw, th, 0, idx), table_r(tab, tw, th, 1, idx), table_r(tab, tw, th, 2, idx));
                 v3 wv = mk3(u - (float)di, v - (float)dj, w - (float)dk);
                 float fi = (float)di, fj = (float)dj, fk = (float)dk;
                 accum += (fi * uu + (1.0f - fi) * (1.0f - uu)) * (fj * vv + (1.0f - fj) * (1.0f - vv)) *
@@ -570,10 +579,13 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         if (P.debug_flags & 1) return mk3s(0.5f);   // ablation only (RT_DEBUG_FLAGS), never exact
         float scale = ((float)detail_i / 4095.0f) * 100.0f;
         float accum = 0.0f, weight = 1.0f;
+        const float* tab = (P.perlin_lds >= 0 && (index & 7) == P.perlin_slot)
+                               ? reinterpret_cast<const float*>(rt_dyn_lds + P.perlin_lds)
+                               : reinterpret_cast<const float*>(T.is_float ? T.data : nullptr);
         v3 q = p;
 #pragma unroll 1
         for (int o = 0; o < 7; o++) {
-            accum += weight * perlin_noise(T, q);
+            accum += weight * perlin_noise(tab, T.w, T.h, q);
             weight *= 0.5f;
             q = scale3(q, 2.0f);
         }
@@ -1517,6 +1529,12 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
     } else if (LDSN) {
         const float4* g = reinterpret_cast<const float4*>(P.nodes);
         for (int k = tid; k < 2 * P.n_nodes; k += BLOCK) s_nodes[k] = g[k];
+        if (P.perlin_lds >= 0) {   // the Perlin table after the nodes (host-sized launch)
+            const rt_dtex& T = P.tex[P.perlin_slot];
+            const float* src = reinterpret_cast<const float*>(T.data);
+            float* dst = reinterpret_cast<float*>(s_nodes + P.perlin_lds);
+            for (int k = tid; k < T.w * T.h; k += BLOCK) dst[k] = src[k];
+        }
     }
     if (LDSN || STATS) __syncthreads();
     if (STATS) t_begin = clock64();
@@ -1937,6 +1955,8 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
     size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
     bool fits = lds <= RT_LDS_NODE_BYTES;
+    // default shapes (0, 30): + the Perlin table the host placed after the nodes
+    const size_t lds_p = lds + (a.perlin_lds >= 0 ? (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h * 4 : 0);
     int rc;
     switch (a.variant) {
         case 10: rc = fits ? launch_persistent(render_persistent<1, 4, false, true, 512>, 512, lds, d, st)
@@ -1962,7 +1982,7 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
                            : launch_persistent(render_persistent<3, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
         case 34: rc = fits ? launch_persistent(render_persistent<7, 5, false, true, 640, 0, 0>, 640, lds, d, st)
                            : launch_persistent(render_persistent<7, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
-        case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds, d, st)
+        case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds_p, d, st)
                            : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
         case 60:   // exact near-first walk (trace_fast), otherwise as 0
         case 68:   // stats twin of 60
@@ -1994,10 +2014,10 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
         }
         default:   // 0: variant 30 specialised for the launch's work split
             if (a.samples)
-                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2>, 512, lds, d, st)
+                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2>, 512, lds_p, d, st)
                           : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2>, 512, 0, d, st);
             else
-                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1>, 512, lds, d, st)
+                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1>, 512, lds_p, d, st)
                           : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1>, 512, 0, d, st);
             break;
     }
