@@ -212,7 +212,12 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "bytes_per_sample": round(bps, 1), "kernel": "render_persistent",
-                    "avg_launch_ms": round(avg_launch_ms, 3), "samples_per_launch": samples_per_launch}
+                    "avg_launch_ms": round(avg_launch_ms, 3), "samples_per_launch": samples_per_launch,
+                    "dram_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
+                    "note": "achieved = the reference's logical record bytes (SURVEY 8d) per launch / launch time; "
+                            "the scene is LDS/L2-resident, so frac > 1 means not HBM-bound (dram_gbs = measured "
+                            "DRAM traffic rate); the limiter is memory latency under divergence at 4 waves/SIMD "
+                            "(DESIGN.md section 4, profiles/r01_region_stats_v0.log)"}
 
     out = {
         "metric": "Msamples/sec (W×H×spp/s) on Book-2 final scene @1080p, 1/2/4/8 GPUs",
