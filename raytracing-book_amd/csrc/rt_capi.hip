@@ -943,6 +943,16 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         (size_t)c->n_dnodes * sizeof(rt_dnode) + (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] * 4 <=
             RT_LDS_NODE_BYTES)
         a.perlin_lds = 2 * c->n_dnodes;
+    // media records (+ sphere boundary) after it, for the same shapes (3 float4 per medium)
+    a.n_media = (int)(c->host_buf[RT_BIND_MEDIA].size() / sizeof(rt_medium));
+    a.media_lds = -1;
+    {
+        const size_t base = (size_t)2 * c->n_dnodes +
+                            (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] / 4 : 0);
+        if (a.n_media > 0 && a.n_media <= 64 && (c->variant == 0 || c->variant == 30) &&
+            (base + 3 * (size_t)a.n_media) * 16 <= RT_LDS_NODE_BYTES)
+            a.media_lds = (int)base;
+    }
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
     a.max_depth = c->max_depth;

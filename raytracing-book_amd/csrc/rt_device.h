@@ -90,6 +90,9 @@ struct rt_kernel_args {
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1
     int perlin_lds;              // its float4 offset in the dynamic LDS (after the nodes), or -1
+    int n_media;
+    int media_lds;               // float4 offset of the media records + sphere boundaries in LDS (3 float4
+                                 // per medium, after the Perlin table), or -1
     int spec_ok;                 // BVH boxes nest (child inside parent): speculative walk allowed
     // exact near-first walk (variant 60; tables from rt_capi.hip build_fast)
     const float4* fnodes;        // 8 octant layouts x n_fnodes threaded SAH nodes (rt_dnode), near child first

@@ -30,6 +30,10 @@ namespace {
 
 typedef rt_kernel_args KP;
 
+// The kernels' dynamic LDS (render_persistent stages the BVH there, then the
+// Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
+extern __shared__ float4 rt_dyn_lds[];
+
 __device__ __forceinline__ v3 f3(float4 v) { return mk3(v.x, v.y, v.z); }
 
 // ---- diagnostic statistics (stats variants only; never in a timed build) ----
@@ -196,15 +200,13 @@ __device__ __noinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3
     return false;
 }
 
-// hitting.glsl:165-168 — the medium's two boundary hits (no rand() yet).
-__device__ __forceinline__ bool medium_bounds(const KP& P, const rt_medium& m, v3 o, v3 d, float a, float time,
-                                              float& t1, float& t2) {
-    if (m.boundary_type == RT_MODEL_SPHERE) {
-        // Both boundary hit_sphere calls (:165, :168) see the same ray and sphere:
-        // the quadratic and both roots are computed once, then each call's root
-        // selection is applied to its own interval.
-        const float4* sp = reinterpret_cast<const float4*>(P.spheres + m.boundary_idx);
-        float4 A = sp[0], B = sp[1];
+// hitting.glsl:165-168 for a sphere boundary (A, B = the sphere's first two float4).
+// Both boundary hit_sphere calls (:165, :168) see the same ray and sphere: the
+// quadratic and both roots are computed once, then each call's root selection
+// is applied to its own interval.
+__device__ __forceinline__ bool sphere_bounds(float4 A, float4 B, v3 o, v3 d, float a, float time, float& t1,
+                                              float& t2) {
+    {
         v3 center = add3(f3(A), scale3(f3(B), time));
         v3 oc = sub3(o, center);
         float half_b = g_dot(oc, d);
@@ -222,6 +224,15 @@ __device__ __forceinline__ bool medium_bounds(const KP& P, const rt_medium& m, v
         else if (lo2 < r_hi && r_hi < RT_INFINITY) t2 = r_hi;
         else return false;
         return true;
+    }
+}
+
+// hitting.glsl:165-168 — the medium's two boundary hits (no rand() yet).
+__device__ __forceinline__ bool medium_bounds(const KP& P, const rt_medium& m, v3 o, v3 d, float a, float time,
+                                              float& t1, float& t2) {
+    if (m.boundary_type == RT_MODEL_SPHERE) {
+        const float4* sp = reinterpret_cast<const float4*>(P.spheres + m.boundary_idx);
+        return sphere_bounds(sp[0], sp[1], o, d, a, time, t1, t2);
     }
     if (!boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, -RT_INFINITY, RT_INFINITY, t1)) return false;
     return boundary_t(P, m.boundary_idx, m.boundary_type, o, d, a, time, t1 + 0.0001f, RT_INFINITY, t2);
@@ -245,9 +256,25 @@ __device__ __forceinline__ bool medium_tail(float neg_inv_density, float t1, flo
 // hitting.glsl:162-193 — returns the hit distance t.
 __device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin,
                                             float tmax, float& rf, float px, float py, float& t) {
-    const rt_medium m = P.media[idx];
     float t1, t2;
-    if (!medium_bounds(P, m, o, d, a, time, t1, t2)) return false;
+    rt_medium m;
+    if (P.media_lds >= 0) {   // the record and its sphere boundary from LDS (render_persistent)
+        const float4* r = rt_dyn_lds + P.media_lds + 3 * idx;
+        const float4 R0 = r[0];
+        m.boundary_idx = __float_as_int(R0.x);
+        m.boundary_type = __float_as_int(R0.y);
+        m.neg_inv_density = R0.z;
+        m.phase_material = __float_as_int(R0.w);
+        m.texture_id = 0;
+        if (m.boundary_type == RT_MODEL_SPHERE) {
+            if (!sphere_bounds(r[1], r[2], o, d, a, time, t1, t2)) return false;
+        } else if (!medium_bounds(P, m, o, d, a, time, t1, t2)) {
+            return false;
+        }
+    } else {
+        m = P.media[idx];
+        if (!medium_bounds(P, m, o, d, a, time, t1, t2)) return false;
+    }
     return medium_tail(m.neg_inv_density, t1, t2, a, tmin, tmax, rf, px, py, t);
 }
 
@@ -487,10 +514,6 @@ __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
     texel(T, x, y, t);
     return t[0];
 }
-
-// The kernels' dynamic LDS (render_persistent stages the BVH there, and the
-// Perlin table after it when P.perlin_lds >= 0).
-extern __shared__ float4 rt_dyn_lds[];
 
 // texel_r of an R32F table given as a plain pointer (LDS copy or global)
 __device__ __forceinline__ float table_r(const float* tab, int w, int h, int x, int y) {
@@ -1535,6 +1558,18 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             float* dst = reinterpret_cast<float*>(s_nodes + P.perlin_lds);
             for (int k = tid; k < T.w * T.h; k += BLOCK) dst[k] = src[k];
         }
+        if (P.media_lds >= 0) {   // per medium: (boundary idx, type, -1/density, phase), sphere A, B
+            for (int k = tid; k < 3 * P.n_media; k += BLOCK) {
+                const rt_medium& m = P.media[k / 3];
+                float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (k % 3 == 0)
+                    v = make_float4(__int_as_float(m.boundary_idx), __int_as_float(m.boundary_type), m.neg_inv_density,
+                                    __int_as_float(m.phase_material));
+                else if (m.boundary_type == RT_MODEL_SPHERE)
+                    v = reinterpret_cast<const float4*>(P.spheres + m.boundary_idx)[k % 3 - 1];
+                s_nodes[P.media_lds + k] = v;
+            }
+        }
     }
     if (LDSN || STATS) __syncthreads();
     if (STATS) t_begin = clock64();
@@ -1956,7 +1991,8 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
     bool fits = lds <= RT_LDS_NODE_BYTES;
     // default shapes (0, 30): + the Perlin table the host placed after the nodes
-    const size_t lds_p = lds + (a.perlin_lds >= 0 ? (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h * 4 : 0);
+    const size_t lds_p = a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
+                         : lds + (a.perlin_lds >= 0 ? (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h * 4 : 0);
     int rc;
     switch (a.variant) {
         case 10: rc = fits ? launch_persistent(render_persistent<1, 4, false, true, 512>, 512, lds, d, st)
