@@ -939,7 +939,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.perlin_slot = a.perlin_lds = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
-    if (a.perlin_slot >= 0 && (c->variant == 0 || c->variant == 30) &&
+    if (a.perlin_slot >= 0 && (c->variant == 0 || c->variant == 30 || c->variant == 35) &&
         (size_t)c->n_dnodes * sizeof(rt_dnode) + (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] * 4 <=
             RT_LDS_NODE_BYTES)
         a.perlin_lds = 2 * c->n_dnodes;
@@ -949,7 +949,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     {
         const size_t base = (size_t)2 * c->n_dnodes +
                             (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] / 4 : 0);
-        if (a.n_media > 0 && a.n_media <= 64 && (c->variant == 0 || c->variant == 30) &&
+        if (a.n_media > 0 && a.n_media <= 64 && (c->variant == 0 || c->variant == 30 || c->variant == 35) &&
             (base + 3 * (size_t)a.n_media) * 16 <= RT_LDS_NODE_BYTES)
             a.media_lds = (int)base;
     }

@@ -1979,7 +1979,7 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
     const rt_kernel_args* d = (const rt_kernel_args*)dargs;
     // Variants (A/B only; all bit-identical):
-    //   0: variant 30 specialised for direct or chunked launches (SMODE)
+    //   0: variant 30 (35 = 30 specialised for direct or chunked launches, SMODE)
     //   30: while-while, fast slab, branch-free node step, 512 threads / 4 waves per SIMD
     //   31 stats of 30;  10 while-while (exact slab) 512/4w;  19 stats of 10
     //   12 = 30 with global-memory nodes;  15 = 30 at 768 threads / 3 waves
@@ -2048,13 +2048,17 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
                             : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1, 2>, 512, l2, d, st);
             break;
         }
-        default:   // 0: variant 30 specialised for the launch's work split
+        case 35:   // 30 specialised for the launch's work split (SMODE; measured 1 ms slower than 30)
             if (a.samples)
                 rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2>, 512, lds_p, d, st)
                           : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2>, 512, 0, d, st);
             else
                 rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1>, 512, lds_p, d, st)
                           : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1>, 512, 0, d, st);
+            break;
+        default:   // 0: variant 30 (work split chosen at run time)
+            rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds_p, d, st)
+                      : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st);
             break;
     }
     if (rc) return rc;
