@@ -100,6 +100,7 @@ struct rt_ctx {
     int wf_slots = 4 << 20; // wavefront: in-flight paths (env RT_WF_SLOTS)
     int wf_refill = 16;     // wavefront: refill a wave once this many lanes are idle (env RT_WF_REFILL)
     bool uv_always = false;
+    bool boxes_canon = false;   // every box has Box.java's axis-aligned face layout (dboxes[18..20])
     bool validated = false;
     uint64_t last_ns = 0;
     int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
@@ -744,22 +745,34 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
     if (binding == RT_BIND_QUADS || binding == RT_BIND_BOXES) {
         const rt_quad* qs = (const rt_quad*)bytes;
         size_t nq = nbytes / sizeof(rt_quad);   // a box is 6 consecutive quads
-        faces.resize(nq * RT_DFACE_F4);
+        faces.resize(binding == RT_BIND_QUADS ? nq * RT_DFACE_F4 : (nq / 6) * RT_DBOX_F4);
         if (binding == RT_BIND_QUADS) {
             for (size_t k = 0; k < nq; k++) face_record(qs[k], &faces[k * RT_DFACE_F4]);
         } else {
-            // per box: the 6 planes first, then the 6 (A, B) pairs (RT_DBOX_F4 float4)
+            // per box: the 6 planes first, then the 6 (A, B) pairs, then the canonical
+            // planes (RT_DBOX_F4 float4)
+            c->boxes_canon = true;
             for (size_t bx = 0; bx < nq / 6; bx++) {
                 float4* o = &faces[bx * RT_DBOX_F4];
+                float sw[12];
                 for (int i = 0; i < 6; i++) {
                     float4 f[3];
                     face_record(qs[bx * 6 + i], f);
                     o[i] = f[0];
                     o[6 + 2 * i] = f[1];
                     o[7 + 2 * i] = f[2];
+                    // Box.java:32-37 face order: normals along z, x, z, x, y, y
+                    static const int kAx[6] = {2, 0, 2, 0, 1, 1};
+                    const float* n = qs[bx * 6 + i].normal;
+                    const int ax = kAx[i];
+                    if (n[ax] == 0.0f || n[(ax + 1) % 3] != 0.0f || n[(ax + 2) % 3] != 0.0f) c->boxes_canon = false;
+                    sw[2 * i] = n[ax];
+                    sw[2 * i + 1] = qs[bx * 6 + i].d;
                 }
-            }
-        }
+                o[18] = make_float4(sw[0], sw[1], sw[2], sw[3]);
+                o[19] = make_float4(sw[4], sw[5], sw[6], sw[7]);
+                o[20] = make_float4(sw[8], sw[9], sw[10], sw[11]);
+            }        }
     }
     if (binding == RT_BIND_LIGHTS) {
         if (nbytes < 4) return set_err(c, RT_ERR_INVALID_ARG, "lights buffer needs the count word");
@@ -916,6 +929,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     if (c->host_buf[RT_BIND_LIGHTS].size() >= 4) std::memcpy(&lc, c->host_buf[RT_BIND_LIGHTS].data(), 4);
     a.lights_count = lc;
     a.uv_always = c->uv_always;
+    a.boxes_canon = c->boxes_canon ? 1 : 0;
     a.variant = c->variant;
     a.spec_ok = c->spec_ok ? 1 : 0;
     const FastTables& F = c->fast;

@@ -8,7 +8,8 @@
 //   boxes    : rt_box[]    as uploaded (480 B AoS)
 //   dquads   : per quad RT_DFACE_F4 float4: plane (n, d), A = (q_a, q_b, u_a, u_b),
 //              B = (v_a, v_b, delta, axis case) — the intersection-only face record
-//   dboxes   : per box RT_DBOX_F4 float4: the 6 planes, then the 6 (A, B) pairs
+//   dboxes   : per box RT_DBOX_F4 float4: the 6 planes, then the 6 (A, B) pairs, then the
+//              canonical planes (s_i, w_i) x 6 in 3 float4 (boxes_canon, below)
 //   media    : rt_medium[] as uploaded (20 B)
 //   lights   : int32 packed ids
 //   textures : RGB8 expanded to RGBA8 (4 B/texel, aligned), RGBA8, R32F
@@ -24,7 +25,7 @@
 #define RT_MAX_FRAMES_PER_LAUNCH 256
 #define RT_NODE_END 0xFFFFu
 #define RT_DFACE_F4 3    // float4 per dquads record
-#define RT_DBOX_F4 18    // float4 per dboxes record
+#define RT_DBOX_F4 21    // float4 per dboxes record
 #define WF_REC_F4 5      // wavefront queue record (path state), float4
 #define WF_HIT_F4 2      // wavefront hit record, float4
 #define RT_LDS_NODE_BYTES (64 * 1024)   // stage the BVH in LDS when it fits (2 workgroups/CU)
@@ -88,6 +89,8 @@ struct rt_kernel_args {
     unsigned long long wf_total; // path ids: wf_tiles * 64 * n_frames
     int wf_slots, wf_tiles, wf_refill;
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
+    int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
+                                 // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
     int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1
     int perlin_lds;              // its float4 offset in the dynamic LDS (after the nodes), or -1
     int n_media;

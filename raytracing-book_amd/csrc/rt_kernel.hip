@@ -187,6 +187,44 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
     return has;
 }
 
+// box_test for a box with Box.java's axis-aligned layout (P.boxes_canon): face i's
+// normal is s_i along axis z, x, z, x, y, y, so for finite o and d
+// dot(n, d) = s_i*d_k and dot(n, o) = s_i*o_k exactly (the other products are
+// exact zeros; a zero sign differs only where the face is skipped or t is 0 <
+// tmin).  The planes come from the record's compact tail (fb[18..20]).
+__device__ __forceinline__ bool box_test_canon(const float4* __restrict__ fb, v3 o, v3 d, float tmin, float tmax,
+                                               float& t, int& face, float& alpha, float& beta) {
+    const float4 c0 = fb[18], c1 = fb[19], c2 = fb[20];
+    const float sv[6] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z};
+    const float wv[6] = {c0.y, c0.w, c1.y, c1.w, c2.y, c2.w};
+    const float dk[6] = {d.z, d.x, d.z, d.x, d.y, d.y};
+    const float ok[6] = {o.z, o.x, o.z, o.x, o.y, o.y};
+    float ti[6];
+    unsigned cand = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const float denom = sv[i] * dk[i];
+        ti[i] = (wv[i] - sv[i] * ok[i]) / denom;   // unused when |denom| < 1e-8
+        if (!(fabsf(denom) < 1e-8f) && (tmin <= ti[i] && ti[i] <= tmax)) cand |= 1u << i;
+    }
+    bool has = false;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        if ((cand >> i) & 1u) {
+            float al, be;
+            if (ti[i] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[i], al, be)) {
+                tmax = ti[i];
+                t = ti[i];
+                face = i;
+                alpha = al;
+                beta = be;
+                has = true;
+            }
+        }
+    }
+    return has;
+}
+
 // hitting.glsl:148-160 for a medium boundary (only rec.t is read, :165-178).
 // Out of line: only quad/box boundaries (scene 7) come here.
 __device__ __noinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3 d, float a, float time, float tmin,
@@ -335,6 +373,9 @@ template <bool STATS>
 __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a, float time,
                                            float tmin, float& tmax, float& rf, float px, float py, Hit& h, bool& has,
                                            unsigned long long* st) {
+    // finite origin and direction: the canonical box planes equal the reference's dot products
+    const bool fin = fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY &&
+                     fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY;
 #pragma unroll 1
     for (int s = 0; s < 2; s++) {
         int ty = (int)((meta >> (16 + 4 * s)) & 0xFu);
@@ -355,7 +396,8 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
             hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, tmax, t, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_BOX) {
-            hit = box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be);
+            hit = (P.boxes_canon && fin) ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be)
+                                         : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
             hit = medium_test(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
@@ -809,6 +851,7 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
     // fast slab test equal to the reference's and monotone in the box; -inf and NaN do not
     if (!(inv.x > -INFINITY && inv.y > -INFINITY && inv.z > -INFINITY)) return 1;
     if (!(fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY)) return 8;
+    if (!(fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY)) return 1;
     const float a = g_dot(d, d);
     const float tmin = 0.001f;
     // trackers: boundary of the constrained slot's medium (its exit bounds the
@@ -841,7 +884,8 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
             else if (ty == RT_MODEL_QUAD)
                 hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, RT_INFINITY, t, al, be);
             else if (ty == RT_MODEL_BOX)
-                hit = box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, RT_INFINITY, t, face, al, be);
+                hit = P.boxes_canon ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, RT_INFINITY, t, face, al, be)
+                                    : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, RT_INFINITY, t, face, al, be);
             if (!hit) continue;
             if (t < best) {
                 second = best;
