@@ -967,6 +967,31 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             (base + 3 * (size_t)a.n_media) * 16 <= RT_LDS_NODE_BYTES)
             a.media_lds = (int)base;
     }
+    // variant 36 (one 1024-thread workgroup per CU, all 160 KB of LDS): also the spheres'
+    // intersection data and the canonical box planes
+    a.n_spheres = (int)(c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere));
+    a.n_boxes = (int)(c->host_buf[RT_BIND_BOXES].size() / sizeof(rt_box));
+    a.sph_lds = a.boxc_lds = -1;
+    if (c->variant == 36) {
+        a.perlin_lds = -1;
+        a.media_lds = -1;
+        size_t off = (size_t)2 * c->n_dnodes;
+        if (a.perlin_slot >= 0) {
+            a.perlin_lds = (int)off;
+            off += ((size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] + 3) / 4;
+        }
+        if (a.n_media > 0 && a.n_media <= 64) {
+            a.media_lds = (int)off;
+            off += 3 * (size_t)a.n_media;
+        }
+        a.sph_lds = (int)off;
+        off += 2 * (size_t)a.n_spheres;
+        if (c->boxes_canon) {
+            a.boxc_lds = (int)off;
+            off += 3 * (size_t)a.n_boxes;
+        }
+        if (off * 16 > RT_LDS_CU_BYTES) a.perlin_lds = a.media_lds = a.sph_lds = a.boxc_lds = -1;
+    }
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
     a.max_depth = c->max_depth;

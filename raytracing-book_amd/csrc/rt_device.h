@@ -30,6 +30,7 @@
 #define WF_HIT_F4 2      // wavefront hit record, float4
 #define RT_LDS_NODE_BYTES (64 * 1024)   // stage the BVH in LDS when it fits (2 workgroups/CU)
 #define RT_LDS_FAST_BYTES (80 * 1024)   // variant 61: two-child tree + stacks in LDS (2 workgroups/CU)
+#define RT_LDS_CU_BYTES (160 * 1024)    // variant 36: one workgroup per CU takes all of it
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
 // continues at index+1 (its RIGHT child, which the reference visits first
@@ -93,7 +94,9 @@ struct rt_kernel_args {
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
     int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1
     int perlin_lds;              // its float4 offset in the dynamic LDS (after the nodes), or -1
-    int n_media;
+    int n_media, n_spheres, n_boxes;
+    int sph_lds, boxc_lds;       // variant 36: float4 offsets in LDS of the spheres' first two float4 and the
+                                 // boxes' canonical plane tails (3 float4), or -1
     int media_lds;               // float4 offset of the media records + sphere boundaries in LDS (3 float4
                                  // per medium, after the Perlin table), or -1
     int spec_ok;                 // BVH boxes nest (child inside parent): speculative walk allowed

@@ -192,9 +192,10 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
 // dot(n, d) = s_i*d_k and dot(n, o) = s_i*o_k exactly (the other products are
 // exact zeros; a zero sign differs only where the face is skipped or t is 0 <
 // tmin).  The planes come from the record's compact tail (fb[18..20]).
-__device__ __forceinline__ bool box_test_canon(const float4* __restrict__ fb, v3 o, v3 d, float tmin, float tmax,
-                                               float& t, int& face, float& alpha, float& beta) {
-    const float4 c0 = fb[18], c1 = fb[19], c2 = fb[20];
+__device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, const float4* __restrict__ fb, v3 o,
+                                               v3 d, float tmin, float tmax, float& t, int& face, float& alpha,
+                                               float& beta) {
+    const float4 c0 = pl[0], c1 = pl[1], c2 = pl[2];
     const float sv[6] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z};
     const float wv[6] = {c0.y, c0.w, c1.y, c1.w, c2.y, c2.w};
     const float dk[6] = {d.z, d.x, d.z, d.x, d.y, d.y};
@@ -369,7 +370,7 @@ __device__ __forceinline__ bool aabb_fast(float4 n0, float4 n1, v3 o, v3 inv, fl
 }
 
 // The two prims of a leaf (compute.glsl:247-256), left then right.
-template <bool STATS>
+template <bool STATS, bool LP = false>
 __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a, float time,
                                            float tmin, float& tmax, float& rf, float px, float py, Hit& h, bool& has,
                                            unsigned long long* st) {
@@ -390,13 +391,17 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
         int face = 0;
         bool hit = false;
         if (ty == RT_MODEL_SPHERE) {
-            hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t);
+            hit = sphere_t(LP ? rt_dyn_lds + P.sph_lds + 2 * ix : reinterpret_cast<const float4*>(P.spheres + ix), time,
+                           o, d, a, tmin, tmax, t);
             if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
         } else if (ty == RT_MODEL_QUAD) {
             hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, tmax, t, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_BOX) {
-            hit = (P.boxes_canon && fin) ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be)
+            hit = (P.boxes_canon && fin)
+                      ? box_test_canon((LP && P.boxc_lds >= 0) ? rt_dyn_lds + P.boxc_lds + 3 * ix
+                                                               : P.dboxes + RT_DBOX_F4 * ix + 18,
+                                       P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be)
                                          : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
@@ -415,7 +420,7 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
 // through inner/missed nodes until each holds a hit leaf (or is done), then the
 // leaves are tested together ("while-while").  WHILE_WHILE bit 1 selects the
 // branch-free node step with the NaN-exact min/max slab test.
-template <int WHILE_WHILE, bool STATS>
+template <int WHILE_WHILE, bool STATS, bool LP = false>
 __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ nodes, v3 o, v3 d, float time,
                                       float& rf, float px, float py, Hit& h, unsigned long long* st) {
     if (P.n_nodes == 0) return false;
@@ -492,7 +497,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
             if (!leaf) break;
             unsigned long long t1 = STATS ? clock64() : 0;
             if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-            leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            leaf_prims<STATS, LP>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
             if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
         }
     } else {
@@ -518,7 +523,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
             if (!leaf) break;
             unsigned long long t1 = STATS ? clock64() : 0;
             if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-            leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            leaf_prims<STATS, LP>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
             if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
             i = meta & 0xFFFFu;
         }
@@ -884,7 +889,8 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
             else if (ty == RT_MODEL_QUAD)
                 hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, RT_INFINITY, t, al, be);
             else if (ty == RT_MODEL_BOX)
-                hit = P.boxes_canon ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, RT_INFINITY, t, face, al, be)
+                hit = P.boxes_canon ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix + 18, P.dboxes + RT_DBOX_F4 * ix, o, d,
+                                                     tmin, RT_INFINITY, t, face, al, be)
                                     : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, RT_INFINITY, t, face, al, be);
             if (!hit) continue;
             if (t < best) {
@@ -1194,7 +1200,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 }
 
 // One iteration of ray_color's loop (compute.glsl:304-340).
-template <int WW, bool STATS, int FAST = 0>
+template <int WW, bool STATS, int FAST = 0, bool LP = false>
 __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, Path& S,
                                        float px, float py, v3& result, unsigned long long* st) {
     if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
@@ -1219,10 +1225,10 @@ __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ n
             hit = fh;
         } else {   // the exact walk, from the same rand() state
             S.rf = rf0;
-            hit = trace<WW, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+            hit = trace<WW, STATS, LP>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
         }
     } else {
-        hit = trace<WW, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+        hit = trace<WW, STATS, LP>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
     }
     unsigned long long ts = STATS ? clock64() : 0;
     if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
@@ -1290,7 +1296,7 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
 // running mean afterwards in frame order (the same operations, so the same bits).
 // SMODE: 0 = direct/chunked chosen at run time, 1 = direct only, 2 = chunked
 // only (no running-mean registers live across the frame loop).
-template <int WW, bool STATS, int SMODE = 0, int FAST = 0>
+template <int WW, bool STATS, int SMODE = 0, int FAST = 0, bool LP = false>
 __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, int x,
                                              int lr, int f0, int f1, unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
@@ -1317,7 +1323,7 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
             fresh = false;
         }
         v3 cur;
-        if (bounce<WW, STATS, FAST>(P, nodes, fc, S, fx, fy, cur, st)) {
+        if (bounce<WW, STATS, FAST, LP>(P, nodes, fc, S, fx, fy, cur, st)) {
             if (direct) {
                 int fc = P.first_frame + f;
                 float n1 = (float)(fc - 1), n = (float)fc;
@@ -1556,7 +1562,8 @@ __device__ __forceinline__ void render_pixel_dec(const KP& P, const float4* __re
 // reaches.  A unit is one 8x8 pixel tile x one chunk of the launch's frames
 // (unit = chunk * n_tiles + tile), so a launch over few tiles (a narrow stripe
 // set at N GPUs) still has many more units than resident waves.
-template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0, int SMODE = 0, int FAST = 0>
+template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0, int SMODE = 0, int FAST = 0,
+          bool LP = false>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
@@ -1602,6 +1609,12 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             float* dst = reinterpret_cast<float*>(s_nodes + P.perlin_lds);
             for (int k = tid; k < T.w * T.h; k += BLOCK) dst[k] = src[k];
         }
+        if (P.sph_lds >= 0)   // spheres: center1 + texture, center_vec + radius
+            for (int k = tid; k < 2 * P.n_spheres; k += BLOCK)
+                s_nodes[P.sph_lds + k] = reinterpret_cast<const float4*>(P.spheres + k / 2)[k % 2];
+        if (P.boxc_lds >= 0)   // the boxes' canonical plane tails
+            for (int k = tid; k < 3 * P.n_boxes; k += BLOCK)
+                s_nodes[P.boxc_lds + k] = P.dboxes[(size_t)(k / 3) * RT_DBOX_F4 + 18 + k % 3];
         if (P.media_lds >= 0) {   // per medium: (boundary idx, type, -1/density, phase), sphere A, B
             for (int k = tid; k < 3 * P.n_media; k += BLOCK) {
                 const rt_medium& m = P.media[k / 3];
@@ -1638,7 +1651,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             if (LDSN) render_pixel_dec<DECQ, STATS>(P, s_nodes, xc, lc, f0, f1, valid, st);
             else render_pixel_dec<DECQ, STATS>(P, reinterpret_cast<const float4*>(P.nodes), xc, lc, f0, f1, valid, st);
         } else if (x < P.width && lr < P.local_rows) {
-            render_pixel<WW, STATS, SMODE, FAST>(P, rnodes, fc, x, lr, f0, f1, st);
+            render_pixel<WW, STATS, SMODE, FAST, LP>(P, rnodes, fc, x, lr, f0, f1, st);
         }
     }
     if (STATS) {
@@ -2062,6 +2075,17 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
                            : launch_persistent(render_persistent<3, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
         case 34: rc = fits ? launch_persistent(render_persistent<7, 5, false, true, 640, 0, 0>, 640, lds, d, st)
                            : launch_persistent(render_persistent<7, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
+        case 36: {   // one 1024-thread workgroup per CU: nodes, Perlin, media, spheres, box planes in LDS
+            size_t l36 = (size_t)2 * a.n_nodes;
+            if (a.perlin_lds >= 0) l36 = (size_t)a.perlin_lds + ((size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h + 3) / 4;
+            if (a.media_lds >= 0) l36 = (size_t)a.media_lds + 3 * (size_t)a.n_media;
+            if (a.sph_lds >= 0) l36 = (size_t)a.sph_lds + 2 * (size_t)a.n_spheres;
+            if (a.boxc_lds >= 0) l36 = (size_t)a.boxc_lds + 3 * (size_t)a.n_boxes;
+            rc = (l36 * 16 <= RT_LDS_CU_BYTES && a.sph_lds >= 0)
+                     ? launch_persistent(render_persistent<3, 4, false, true, 1024, 0, 0, 0, true>, 1024, l36 * 16, d, st)
+                     : launch_persistent(render_persistent<3, 4, false, false, 1024>, 1024, 0, d, st);
+            break;
+        }
         case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds_p, d, st)
                            : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
         case 60:   // exact near-first walk (trace_fast), otherwise as 0
