@@ -45,7 +45,8 @@ enum {
     ST_SPH_IT, ST_QUAD_IT, ST_BOX_IT, ST_MED_IT,
     // near-first walk (variants 60/61): traces, those that took the exact walk (and why: 9 reasons),
     // node steps and prim tests
-    ST_FAST_TRACES, ST_FAST_EXACT, ST_FAST_WHY, ST_FAST_STEPS = ST_FAST_WHY + 9, ST_FAST_TESTS, ST_N
+    ST_FAST_TRACES, ST_FAST_EXACT, ST_FAST_WHY, ST_FAST_STEPS = ST_FAST_WHY + 9, ST_FAST_TESTS,
+    ST_FAST_PRE_CYC, ST_FAST_POST_CYC, ST_FAST_EXACT_CYC, ST_N
 };
 __device__ __forceinline__ bool first_active_lane() {
     unsigned long long m = __ballot(1);
@@ -859,6 +860,7 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
     if (!(fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY)) return 1;
     const float a = g_dot(d, d);
     const float tmin = 0.001f;
+    unsigned long long c_pre = STATS ? clock64() : 0;
     // trackers: boundary of the constrained slot's medium (its exit bounds the
     // solids that can be its ray_t.max) and the closest / second closest solid
     // ranked before the slot
@@ -869,6 +871,7 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
     uint32_t ll0 = 0u, ll1 = 0u;
     float pb0 = tb0 ? fprune(t2_0) : -RT_INFINITY;
     float pb1 = tb1 ? fprune(t2_1) : -RT_INFINITY;
+    if (STATS) st_add(st, ST_FAST_PRE_CYC, clock64() - c_pre);
     float best = RT_INFINITY, second = RT_INFINITY, pb = RT_INFINITY;
     int bty = 0, bix = 0, bface = 0;
     float bal = 0.0f, bbe = 0.0f;
@@ -994,6 +997,7 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
         atomicAdd(st + ST_FAST_STEPS, (unsigned long long)n_steps);
         atomicAdd(st + ST_FAST_TESTS, (unsigned long long)n_tests);
     }
+    unsigned long long c_post = STATS ? clock64() : 0;
     if (best < RT_INFINITY) {
         if (second <= fwin(best)) return 2;
         if (!ref_leaf_hit(rn, P.finfo[P.finfo_base[bty] + bix] & 0xFFFFu, o, inv, fwin(best))) return 3;
@@ -1060,6 +1064,7 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
     } else {
         has = false;
     }
+    if (STATS) st_add(st, ST_FAST_POST_CYC, clock64() - c_post);
     return 0;
 }
 
@@ -1224,8 +1229,10 @@ __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ n
         if (why == 0) {
             hit = fh;
         } else {   // the exact walk, from the same rand() state
+            unsigned long long c_ex = STATS ? clock64() : 0;
             S.rf = rf0;
             hit = trace<WW, STATS, LP>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+            if (STATS) st_add(st, ST_FAST_EXACT_CYC, clock64() - c_ex);
         }
     } else {
         hit = trace<WW, STATS, LP>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);

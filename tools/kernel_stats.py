@@ -13,7 +13,7 @@ import rtamd  # noqa: E402
 NAMES = ["TOTAL", "START_CYC", "START_IT", "START_LN", "NODE_CYC", "NODE_IT", "NODE_LN", "LEAF_CYC", "LEAF_IT",
          "LEAF_LN", "SPH_LN", "QUAD_LN", "BOX_LN", "MED_LN", "SHADE_CYC", "SHADE_IT", "SHADE_LN", "SPH_IT",
          "QUAD_IT", "BOX_IT", "MED_IT", "FAST_TRACES", "FAST_EXACT"] + [f"FAST_WHY{r}" for r in range(1, 10)] + [
-         "FAST_STEPS", "FAST_TESTS"]
+         "FAST_STEPS", "FAST_TESTS", "FAST_PRE_CYC", "FAST_POST_CYC", "FAST_EXACT_CYC"]
 
 
 def main():
