@@ -216,7 +216,7 @@ def main():
                     "dram_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
                     "note": "achieved = the reference's logical record bytes (SURVEY 8d) per launch / launch time; "
                             "the scene is LDS/L2-resident, so frac > 1 means not HBM-bound (dram_gbs = measured "
-                            "DRAM traffic rate); the limiter is memory latency under divergence at 4 waves/SIMD "
+                            "DRAM traffic rate); the limiter is VALU issue under divergence (12% of lanes active) at 4 waves/SIMD "
                             "(DESIGN.md section 4, profiles/r01_region_stats_v0.log)"}
 
     out = {
