@@ -29,6 +29,13 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
                          size_t bbytes, int n_spheres, void* nodes_out, size_t nodes_cap, int* n_per_octant,
                          unsigned int* info_out, size_t info_cap, int* slots_out, int* n_slots);
 
+/* Host-only: the link-format copy of a reference BVH upload that the default
+ * kernel stages in LDS (rt_device.h RT_LINK_*): per threaded node two float4
+ * (box, hit / miss successor byte offsets), then the leaves' (types, prims)
+ * as uint2.  *n_f4 = its float4 count, 0 when the BVH has too many nodes for
+ * 16-bit offsets (the kernel then walks the threaded nodes). */
+int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4);
+
 /* Diagnostic build of the render kernel with wave-level region timers and
  * active-lane counters (never used for timed numbers).  enable=1 switches the
  * context to it and zeroes the counters; read returns n <= 64 counters. */

@@ -45,6 +45,7 @@ struct Device {
     DevBuf wf_q[2], wf_hits, wf_ctr;   // wavefront pipeline (variant 50)
     DevBuf fnodes, finfo;    // exact near-first walk tables (variants 60, 61)
     DevBuf f2inner, f2leaves;
+    DevBuf links;            // link-format BVH (variant 37)
     int fast_gen = -1;       // rt_ctx::fast_gen these copies belong to
     unsigned* wf_host_ctr = nullptr;   // pinned readback of the queue counts
     static constexpr int kRing = 8;
@@ -93,6 +94,7 @@ struct rt_ctx {
     int n_dnodes = 0;
     std::vector<rt_dnode> dnodes;   // host copy of the threaded BVH (fast-walk tables are built from it)
     FastTables fast;
+    std::vector<float4> links;   // build_links(dnodes), empty when unavailable
     int fast_gen = 0;
     bool spec_ok = false;   // every child box lies inside its parent's (speculative walk allowed)
     int shade_k = 32;       // decoupled schedule threshold (env RT_SHADE_K)
@@ -271,6 +273,41 @@ bool boxes_nest(const std::vector<rt_dnode>& dn) {
         if (!inside(dn[k + 1], dn[k]) || !inside(dn[l], dn[k])) return false;
     }
     return true;
+}
+
+// The threaded BVH in link format (rt_device.h RT_LINK_*; variant 37's node
+// loop, rt_kernel.hip trace): node k is (xmin, xmax, ymin, ymax), (zmin, zmax,
+// hit successor, miss successor) at byte offset 32 k; an inner node's hit
+// successor is node k + 1, a leaf's leaves the loop with its leaf ordinal and
+// skip offset; the leaves' (types, prims) follow the nodes as uint2.  Same
+// node sequence as the threaded walk.  Empty when the offsets do not fit.
+std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
+    std::vector<float4> out;
+    const size_t n = dn.size();
+    size_t nl = 0;
+    for (const rt_dnode& d : dn) nl += (d.meta & 0xF0000u) != 0;
+    if (n == 0 || n > RT_LINK_MAX_NODES || nl > 0x7FFF) return out;
+    out.assign(2 * n + (nl + 1) / 2, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    uint2* leaves = reinterpret_cast<uint2*>(out.data() + 2 * n);
+    auto f = [](uint32_t u) {
+        float x;
+        std::memcpy(&x, &u, 4);
+        return x;
+    };
+    uint32_t li = 0;
+    for (size_t k = 0; k < n; k++) {
+        const rt_dnode& d = dn[k];
+        const uint32_t skip = d.meta & 0xFFFFu;
+        const uint32_t miss = skip == RT_NODE_END ? RT_LINK_END : 32u * skip;
+        uint32_t hit = 32u * (uint32_t)(k + 1);
+        if ((d.meta & 0xF0000u) != 0) {
+            hit = RT_LINK_LEAF | li << 16 | (skip == RT_NODE_END ? 0xFFFFu : 32u * skip);
+            leaves[li++] = make_uint2(d.meta & 0xFF0000u, d.prims);
+        }
+        out[2 * k] = make_float4(d.xmin, d.xmax, d.ymin, d.ymax);
+        out[2 * k + 1] = make_float4(d.zmin, d.zmax, f(hit), f(miss));
+    }
+    return out;
 }
 
 // ---- exact near-first walk (variant 60; rt_kernel.hip trace_fast) -------------
@@ -623,6 +660,7 @@ int validate(rt_ctx* c) {
     const std::vector<uint8_t>& BB = c->host_buf[RT_BIND_BOXES];
     c->fast = build_fast(c->dnodes, ns, (const rt_quad*)QB.data(), nq, (const rt_box*)BB.data(), nb);
     c->fast.ok = c->fast.ok && c->spec_ok && !c->uv_always;
+    c->links = build_links(c->dnodes);
     c->fast_gen++;
     c->validated = true;
     return RT_OK;
@@ -698,7 +736,7 @@ int rt_destroy(rt_ctx* c) {
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter); dev_free(d.samples);
         dev_free(d.dquads); dev_free(d.dboxes);
         dev_free(d.wf_q[0]); dev_free(d.wf_q[1]); dev_free(d.wf_hits); dev_free(d.wf_ctr);
-        dev_free(d.fnodes); dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves);
+        dev_free(d.fnodes); dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links);
         if (d.wf_host_ctr) (void)hipHostFree(d.wf_host_ctr);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
@@ -949,22 +987,26 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
     a.shade_k = c->shade_k;
     a.debug_flags = c->debug_flags;
-    // Perlin table in LDS after the nodes (default launch shapes only; rt_kernel.hip texture_color)
+    a.n_lnode_f4 = (int)c->links.size();
+    // Perlin table in LDS after the nodes (default launch shapes only; rt_kernel.hip texture_color);
+    // variant 37 stages the link-format nodes (and may use 80 KB)
+    const bool links = (c->variant == 0 || c->variant == 37 || c->variant == 38) && a.n_lnode_f4 > 0;
+    const bool shape_p = c->variant == 0 || c->variant == 30 || c->variant == 35 || c->variant == 37 || c->variant == 38;
+    const size_t node_f4 = links ? (size_t)a.n_lnode_f4 : (size_t)2 * c->n_dnodes;
+    const size_t lds_cap = links ? RT_LDS_FAST_BYTES : RT_LDS_NODE_BYTES;
     a.perlin_slot = a.perlin_lds = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
-    if (a.perlin_slot >= 0 && (c->variant == 0 || c->variant == 30 || c->variant == 35) &&
-        (size_t)c->n_dnodes * sizeof(rt_dnode) + (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] * 4 <=
-            RT_LDS_NODE_BYTES)
-        a.perlin_lds = 2 * c->n_dnodes;
+    if (a.perlin_slot >= 0 && shape_p &&
+        node_f4 * 16 + (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] * 4 <= lds_cap)
+        a.perlin_lds = (int)node_f4;
     // media records (+ sphere boundary) after it, for the same shapes (3 float4 per medium)
     a.n_media = (int)(c->host_buf[RT_BIND_MEDIA].size() / sizeof(rt_medium));
     a.media_lds = -1;
     {
-        const size_t base = (size_t)2 * c->n_dnodes +
+        const size_t base = node_f4 +
                             (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] / 4 : 0);
-        if (a.n_media > 0 && a.n_media <= 64 && (c->variant == 0 || c->variant == 30 || c->variant == 35) &&
-            (base + 3 * (size_t)a.n_media) * 16 <= RT_LDS_NODE_BYTES)
+        if (a.n_media > 0 && a.n_media <= 64 && shape_p && (base + 3 * (size_t)a.n_media) * 16 <= lds_cap)
             a.media_lds = (int)base;
     }
     // variant 36 (one 1024-thread workgroup per CU, all 160 KB of LDS): also the spheres'
@@ -1036,6 +1078,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             if (!rf) rf = dev_alloc_copy(c, d, d.finfo, F.info.data(), F.info.size() * sizeof(uint32_t));
             if (!rf) rf = dev_alloc_copy(c, d, d.f2inner, F.inner2.data(), F.inner2.size() * sizeof(float4));
             if (!rf) rf = dev_alloc_copy(c, d, d.f2leaves, F.leaves2.data(), F.leaves2.size() * sizeof(uint2));
+            if (!rf) rf = dev_alloc_copy(c, d, d.links, c->links.data(), c->links.size() * sizeof(float4));
             if (rf) return rf;
             d.fast_gen = c->fast_gen;
         }
@@ -1043,6 +1086,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         a.finfo = (const uint32_t*)d.finfo.ptr;
         a.f2inner = (const float4*)d.f2inner.ptr;
         a.f2leaves = (const uint2*)d.f2leaves.ptr;
+        a.lnodes = (const float4*)d.links.ptr;
         a.n_pixels = (size_t)d.local_rows * c->width;
         // Frames per launch and the unit split.  Units = tiles x chunks; with too
         // few tiles per resident wave (small images, N-GPU stripes) the frames
@@ -1253,6 +1297,21 @@ int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t ou
     return RT_OK;
 }
 
+int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4) {
+    if (!bvh || !n_f4 || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
+    std::vector<rt_dnode> dn;
+    rt_ctx tmp;
+    int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
+    if (r) return r;
+    const std::vector<float4> L = build_links(dn);
+    *n_f4 = (int)L.size();
+    if (out) {
+        if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
+        std::memcpy(out, L.data(), L.size() * sizeof(float4));
+    }
+    return RT_OK;
+}
+
 int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size_t qbytes, const void* boxes,
                          size_t bbytes, int n_spheres, void* nodes_out, size_t nodes_cap, int* n_per_octant,
                          uint32_t* info_out, size_t info_cap, int* slots_out, int* n_slots) {
@@ -1297,10 +1356,10 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
         if (d.stats.ptr) HIPCHK(c, hipMemsetAsync(d.stats.ptr, 0, d.stats.bytes, d.stream));
         HIPCHK(c, hipStreamSynchronize(d.stream));
     }
-    // stats twin of the current launch shape: 0/12/15/30 -> 31, 10 -> 19
+    // stats twin of the current launch shape: 12/15/30 -> 31, 10 -> 19, 0/37 -> 38
     if (on) {
         int v = c->variant;
-        c->variant = (v == 10 || v == 19) ? 19 : (v >= 40 && v < 50) ? 49 : (v == 60 || v == 68) ? 68 : (v == 61 || v == 69) ? 69 : 31;
+        c->variant = (v == 10 || v == 19) ? 19 : (v >= 40 && v < 50) ? 49 : (v == 60 || v == 68) ? 68 : (v == 61 || v == 69) ? 69 : (v == 0 || v == 37 || v == 38) ? 38 : 31;
     } else {
         c->variant = 0;
     }

@@ -45,6 +45,15 @@ struct rt_dnode {
 };
 static_assert(sizeof(rt_dnode) == 32, "device node is 32 B");
 
+// Link format of the same nodes (variant 37): word 6 / 7 of a node are the
+// successors on a box hit / miss as byte offsets into the node array, so the
+// node loop is one select.  A hit leaf's successor leaves the loop:
+// RT_LINK_LEAF | leaf << 16 | the skip offset (0xFFFF = end of walk); the end
+// of the walk is RT_LINK_END.  Both have the sign bit set.
+#define RT_LINK_LEAF 0x80000000u
+#define RT_LINK_END 0xFFFFFFFFu
+#define RT_LINK_MAX_NODES 2047   // offsets (32 B per node) fit 16 bits below 0xFFFF
+
 struct rt_dtex {
     const void* data;   // RGBA8 (uint32) or R32F
     int w, h;
@@ -113,6 +122,9 @@ struct rt_kernel_args {
     const float4* f2inner;       // 4 float4 per inner node: left box, right box, refs + tracker bits
     const uint2* f2leaves;       // (meta, prims) per leaf
     int n_f2inner, n_f2leaves, f2depth;
+    // the reference's threaded BVH with explicit successors (variant 37; rt_capi.hip build_links)
+    const float4* lnodes;        // 2 float4 per node, then the leaves' (types, prims) as uint2
+    int n_lnode_f4;              // float4 of the whole array; 0 = not available (too many nodes)
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
 };
 

@@ -370,6 +370,18 @@ __device__ __forceinline__ bool aabb_fast(float4 n0, float4 n1, v3 o, v3 inv, fl
     return !(hi <= lo);
 }
 
+// aabb_fast with the six slab subtractions and products as packed pairs
+// (v_pk_add_f32 / v_pk_mul_f32: the same IEEE roundings, half the issue).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bool aabb_pk(float4 n0, float4 n1, v3 o, v3 inv, float tmin, float tmax) {
+    const f2v tx = (f2v{n0.x, n0.y} - f2v{o.x, o.x}) * f2v{inv.x, inv.x};
+    const f2v ty = (f2v{n0.z, n0.w} - f2v{o.y, o.y}) * f2v{inv.y, inv.y};
+    const f2v tz = (f2v{n1.x, n1.y} - f2v{o.z, o.z}) * f2v{inv.z, inv.z};
+    float lo = v_max(v_max3(tmin, v_min(tx.x, tx.y), v_min(ty.x, ty.y)), v_min(tz.x, tz.y));
+    float hi = v_min(v_min3(tmax, v_max(tx.x, tx.y), v_max(ty.x, ty.y)), v_max(tz.x, tz.y));
+    return !(hi <= lo);
+}
+
 // The two prims of a leaf (compute.glsl:247-256), left then right.
 template <bool STATS, bool LP = false>
 __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a, float time,
@@ -433,6 +445,43 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
     // rays that need the exact slab (see aabb_fast); wave-uniform fast path otherwise
     const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
     const bool wave_exact = (WHILE_WHILE & 2) ? (__ballot(lane_exact) != 0) : true;   // uniform
+    if (WHILE_WHILE & 8) {
+        // link-format nodes (rt_device.h RT_LINK_*): the successor is one select
+        // between the node's hit and miss words; a hit leaf or the end leaves
+        // the loop (sign bit)
+        const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
+        const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
+        uint32_t nx = 0u;
+        for (;;) {
+            unsigned long long t0 = STATS ? clock64() : 0;
+            while ((int)nx >= 0) {
+                if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
+                const float4 n0 = *reinterpret_cast<const float4*>(base + nx);
+                const float4 n1 = *reinterpret_cast<const float4*>(base + nx + 16);
+                bool hitn;
+                if (!wave_exact) {
+                    hitn = aabb_pk(n0, n1, o, inv, tmin, tmax);
+                } else {
+                    float lo = tmin, hi = tmax;
+                    slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+                    slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+                    slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+                    hitn = !(hi <= lo);
+                }
+                nx = __float_as_uint(hitn ? n1.z : n1.w);
+            }
+            if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
+            if (nx == RT_LINK_END) break;
+            unsigned long long t1 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+            const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
+            leaf_prims<STATS, LP>(P, lf.x, lf.y, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+            nx &= 0xFFFFu;
+            if (nx == 0xFFFFu) break;
+        }
+        return has;
+    }
     if (WHILE_WHILE & 2) {
         // while-while with a branch-free node step and one loop exit: a hit inner
         // node continues at i+1 (its right child), anything else at the skip
@@ -1608,8 +1657,9 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             fc.stack = reinterpret_cast<short*>(s_nodes) + tid;
         }
     } else if (LDSN) {
-        const float4* g = reinterpret_cast<const float4*>(P.nodes);
-        for (int k = tid; k < 2 * P.n_nodes; k += BLOCK) s_nodes[k] = g[k];
+        const float4* g = (WW & 8) ? P.lnodes : reinterpret_cast<const float4*>(P.nodes);
+        const int nf4 = (WW & 8) ? P.n_lnode_f4 : 2 * P.n_nodes;
+        for (int k = tid; k < nf4; k += BLOCK) s_nodes[k] = g[k];
         if (P.perlin_lds >= 0) {   // the Perlin table after the nodes (host-sized launch)
             const rt_dtex& T = P.tex[P.perlin_slot];
             const float* src = reinterpret_cast<const float*>(T.data);
@@ -2043,8 +2093,10 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
     const rt_kernel_args* d = (const rt_kernel_args*)dargs;
     // Variants (A/B only; all bit-identical):
-    //   0: variant 30 (35 = 30 specialised for direct or chunked launches, SMODE)
+    //   0: variant 37 (30 when the link format is unavailable or does not fit LDS)
+    //   37: 30 over the link-format nodes (explicit hit / miss successors, packed slab); 38 stats of 37
     //   30: while-while, fast slab, branch-free node step, 512 threads / 4 waves per SIMD
+    //   35 = 30 specialised for direct or chunked launches (SMODE)
     //   31 stats of 30;  10 while-while (exact slab) 512/4w;  19 stats of 10
     //   12 = 30 with global-memory nodes;  15 = 30 at 768 threads / 3 waves
     if (a.variant == 50) {
@@ -2057,6 +2109,10 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     // default shapes (0, 30): + the Perlin table the host placed after the nodes
     const size_t lds_p = a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
                          : lds + (a.perlin_lds >= 0 ? (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h * 4 : 0);
+    // variant 37: link-format nodes, then the Perlin table and media as placed by the host
+    const size_t lds_l = a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
+                         : a.perlin_lds >= 0 ? ((size_t)a.perlin_lds + (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h / 4) * 16
+                                             : (size_t)a.n_lnode_f4 * 16;
     int rc;
     switch (a.variant) {
         case 10: rc = fits ? launch_persistent(render_persistent<1, 4, false, true, 512>, 512, lds, d, st)
@@ -2093,6 +2149,17 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
                      : launch_persistent(render_persistent<3, 4, false, false, 1024>, 1024, 0, d, st);
             break;
         }
+        default:   // 0 = 37
+        case 37:   // 30 over the link-format nodes in LDS (up to 80 KB with the Perlin table and media)
+        case 38:   // stats twin
+            if (a.n_lnode_f4 > 0 && lds_l <= RT_LDS_FAST_BYTES) {
+                rc = a.variant == 38 ? launch_persistent(render_persistent<11, 4, true, true, 512>, 512, lds_l, d, st)
+                                     : launch_persistent(render_persistent<11, 4, false, true, 512>, 512, lds_l, d, st);
+                break;
+            }
+            rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds_p, d, st)
+                      : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st);
+            break;
         case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds_p, d, st)
                            : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
         case 60:   // exact near-first walk (trace_fast), otherwise as 0
@@ -2130,10 +2197,6 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
             else
                 rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1>, 512, lds_p, d, st)
                           : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1>, 512, 0, d, st);
-            break;
-        default:   // 0: variant 30 (work split chosen at run time)
-            rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds_p, d, st)
-                      : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st);
             break;
     }
     if (rc) return rc;

@@ -93,6 +93,7 @@ def amd():
         _proto(L, "rt_debug_threaded_bvh", i, vp, sz, vp, sz, c_int_p)
         _proto(L, "rt_debug_fast_tables", i, vp, sz, vp, sz, vp, sz, i, vp, sz, c_int_p,
                ctypes.POINTER(ctypes.c_uint32), sz, c_int_p, c_int_p)
+        _proto(L, "rt_debug_link_nodes", i, vp, sz, vp, sz, c_int_p)
         _proto(L, "rt_debug_device_count", i)
         _proto(L, "rt_debug_enable_stats", i, vp, i)
         _proto(L, "rt_debug_read_stats", i, vp, ctypes.POINTER(ctypes.c_ulonglong), i)

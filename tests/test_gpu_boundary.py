@@ -137,7 +137,7 @@ def test_bound_torch_image_and_stream(gpu):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
-VARIANTS = [0, 10, 12, 15, 30, 32, 35, 36, 41, 42, 43, 50, 60, 61]
+VARIANTS = [0, 10, 12, 15, 30, 32, 35, 36, 37, 41, 42, 43, 50, 60, 61]
 
 
 @pytest.mark.parametrize("chunk_target", ["0", "1", "16", "100000"])
