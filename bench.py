@@ -3,14 +3,30 @@
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
 it is launched under torch.distributed.run, one rank per GPU.  A *step* is one
-pass of the hot path over one batch: every pixel of the 1920x1080 scene-8 image
-advanced by F progressive frames (F samples per pixel), through rt_render.
-With N ranks the image rows are split into interleaved stripes and each step
-advances F*N frames, so every rank does a fixed 1920x1080xF samples per step
-(weak scaling).  value = all ranks' samples / max-over-ranks wall time of the
-K timed steps.  Inputs (scene buffers, image) are resident in HBM before the
-timed region.  The rank-0 JSON line carries the HIP-event kernel roofline and
-the CPU-oracle baseline (on a bounded sample).
+pass of the hot path over one batch: every pixel of the image advanced by F
+progressive frames (F samples per pixel) through rt_render.  With N ranks the
+image rows are split into interleaved stripes and each step advances F*N
+frames, so every rank does a fixed W x H x F samples per step (weak scaling).
+value = all ranks' samples / max-over-ranks wall time of the K timed steps.
+Inputs (scene buffers, image) are resident in HBM before the timed region.
+
+Workloads (BASELINE.json configs; --preset, default c3 = the metric's config):
+  c2  scene 0 (Book-1 final), 1920x1080, sqrt_spp for 1024 spp
+  c3  scene 8 (Book-2 final), 1920x1080, sqrt_spp for 4096 spp   <- headline
+  c4  scene 6 (Book-3 Cornell box), 1920x1080, sqrt_spp for 4096 spp
+  c5  scene 8, 3840x2160, sqrt_spp for 8192 spp (the 8-GPU config)
+max_depth 5 (the reference CLI default, Main.java:37) unless --depth.
+
+The rank-0 JSON line carries
+  * roofline: the render kernel against the VALU issue ceiling (bound "valu"):
+    achieved = SQ_INSTS_VALU per launch (rocprofv3 PMC, committed in
+    profiles/valu.json for this config) / the launch time measured here with
+    HIP events on the kernel's stream; peak = 1024 SIMDs x 2.4 GHz / 2 cycles
+    per wave64 VALU instruction (MI355X_MICROARCH.md:54,473; the microkernel
+    tools/valu_peak.hip measures the 4-waves-per-SIMD ceiling, also reported);
+  * cpu_baseline: the CPU oracle (oracle/, a restatement of the reference's
+    GLSL; the reference has no CPU path) with one thread per host CPU, >= 60 s,
+    on a bounded stripe of the same workload, plus the C1 CPU config in full.
 """
 import argparse
 import json
@@ -25,7 +41,18 @@ sys.path.insert(0, os.path.join(REPO, "raytracing-book_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector
+SIMDS = 1024                   # 256 CUs x 4 SIMD-32
+CLOCK_HZ = 2.4e9               # max clock
+CYCLES_PER_VALU = 2.0          # wave64 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md:54,473)
+VALU_PEAK = SIMDS * CLOCK_HZ / CYCLES_PER_VALU / 1e9   # 1228.8 G wave-instructions/s
+METRIC = "Msamples/sec (W×H×spp/s) on Book-2 final scene @1080p, 1/2/4/8 GPUs"
+
+PRESETS = {
+    "c2": dict(scene=0, width=1920, height=1080, spp_total=1024, name="C2 scene0 Book-1 final"),
+    "c3": dict(scene=8, width=1920, height=1080, spp_total=4096, name="C3 scene8 Book-2 final"),
+    "c4": dict(scene=6, width=1920, height=1080, spp_total=4096, name="C4 scene6 Book-3 Cornell box"),
+    "c5": dict(scene=8, width=3840, height=2160, spp_total=8192, name="C5 scene8 Book-2 final 4K"),
+}
 
 
 def log(*a):
@@ -37,65 +64,160 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=8)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--scene", type=int, default=8)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--preset", default="c3", choices=sorted(PRESETS))
+    p.add_argument("--scene", type=int, default=None)
+    p.add_argument("--width", type=int, default=None)
+    p.add_argument("--height", type=int, default=None)
+    p.add_argument("--spp-total", type=int, default=None, help="sqrt_spp uniform (the config's spp)")
     p.add_argument("--frames-per-step", type=int, default=64, help="spp per step per rank")
     p.add_argument("--depth", type=int, default=5)
-    p.add_argument("--spp-total", type=int, default=4096, help="sqrt_spp uniform (BASELINE C3: 4096)")
     p.add_argument("--stripe-rows", type=int, default=8)
     p.add_argument("--seed", type=int, default=1)
-    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--cpu-seconds", type=float, default=60.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--png", default=None)
-    return p.parse_args()
+    a = p.parse_args()
+    pre = PRESETS[a.preset]
+    for k in ("scene", "width", "height", "spp_total"):
+        if getattr(a, k) is None:
+            setattr(a, k, pre[k])
+    a.workload_name = pre["name"] if all(getattr(a, k) == pre[k] for k in ("scene", "width", "height", "spp_total")) \
+        else f"scene{a.scene}"
+    return a
+
+
+def config_key(a, frames):
+    return f"scene{a.scene}_{a.width}x{a.height}_f{frames}_d{a.depth}"
+
+
+# ---------------------------------------------------------------- CPU baseline
+def host_facts():
+    model, sockets, cores_per = "unknown", set(), None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k = k.strip()
+                if k == "model name" and model == "unknown":
+                    model = v.strip()
+                elif k == "physical id":
+                    sockets.add(v.strip())
+                elif k == "cpu cores" and cores_per is None:
+                    cores_per = int(v)
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    phys = (len(sockets) or 1) * cores_per if cores_per else None
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "physical_cores": phys,
+            "cgroup_cpu_quota": quota}
+
+
+def _oracle_rate(pyoracle, rtamd, osc, W, H, rows_rank, rows_world, stripe, seed, seconds, threads):
+    """Frames of the rows of one stripe set, in growing chunks, until `seconds`."""
+    image = np.zeros((H, W, 4), np.float32)
+    rows = rtamd.local_rows(H, rows_rank, rows_world, stripe)
+    nf, chunk, dt = 0, 1, 0.0
+    while dt < seconds and nf < 1 << 20:
+        rf = rtamd.frame_rand_factors(seed, nf, chunk)
+        t = time.perf_counter()
+        pyoracle.render(osc, rf, first_frame=nf + 1, image=image, rank=rows_rank, world=rows_world,
+                        stripe_rows=stripe, nthreads=threads)
+        dt += time.perf_counter() - t
+        nf += chunk
+        chunk = max(1, min(2 * chunk, int((seconds - dt) / (dt / nf)) if dt < seconds else 1))
+    return W * rows * nf, nf, rows, dt
 
 
 def cpu_baseline(scene, args):
-    """CPU oracle (oracle/, the build's scalar restatement; the reference has no
-    CPU path) timed on this host over a bounded sample of the same
-    workload: the full-width rows of stripe 0 of 8 (1/8 of the image), as many
-    frames as fit in ~cpu_seconds.  The rate does not depend on spp."""
+    """CPU oracle (oracle/, the build's scalar restatement of compute.glsl; the
+    reference has no CPU path) on this host.  One thread per host
+    CPU, >= args.cpu_seconds on the full-width rows of stripe 0 of 8 of the same
+    workload; the rate does not depend on spp.  Also: a 1-thread rate, the C1
+    config (scene 9, 400x225, 64 spp, depth 8) rendered in full, and the host
+    facts (the job's cgroup CPU quota caps what many threads can get)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     import rtamd
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    facts = host_facts()
+    threads = facts["nproc"] or 1
     osc = pyoracle.OracleScene(scene, max_depth=args.depth, spp=args.spp_total)
     W, H = scene.width, scene.height
-    world_s = 8
-    rows = rtamd.local_rows(H, 0, world_s, args.stripe_rows)
-    image = np.zeros((H, W, 4), np.float32)
-    # frames in growing chunks (progressive accumulation continues) until ~cpu_seconds
-    nf, chunk, dt = 0, 1, 0.0
-    while dt < args.cpu_seconds and nf < 65536:
-        rf = rtamd.frame_rand_factors(args.seed, nf, chunk)
-        t = time.perf_counter()
-        pyoracle.render(osc, rf, first_frame=nf + 1, image=image, rank=0, world=world_s,
-                        stripe_rows=args.stripe_rows, nthreads=threads)
-        dt += time.perf_counter() - t
-        nf += chunk
-        chunk = max(1, min(2 * chunk, int((args.cpu_seconds - dt) / (dt / nf)) if dt < args.cpu_seconds else 1))
-    samples = W * rows * nf
+    samples, nf, rows, dt = _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 8, args.stripe_rows, args.seed,
+                                         args.cpu_seconds, threads)
+    s1, nf1, rows1, dt1 = _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 64, args.stripe_rows, args.seed,
+                                       min(10.0, args.cpu_seconds), 1)
+    # C1 (BASELINE.json configs[0]): the CPU reference path's own config, in full
+    c1 = rtamd.Scene(9, 400, 225, seed=args.seed)
+    oc1 = pyoracle.OracleScene(c1, max_depth=8, spp=64)
+    rf = rtamd.frame_rand_factors(args.seed, 0, 64)
+    t = time.perf_counter()
+    pyoracle.render(oc1, rf, first_frame=1, nthreads=threads)
+    c1_s = time.perf_counter() - t
+    eff = facts["cgroup_cpu_quota"] or facts["affinity_cpus"]
+    per_thread = s1 / dt1 / 1e6
     return {
         "value": round(samples / dt / 1e6, 3),
         "unit": "Msamples/s",
-        "cores": threads,
+        "cores": int(round(eff)) if eff else threads,
         "kind": "port",
-        "sample": f"scene {args.scene} {W}x{H} max_depth {args.depth}: rows of stripe 0/{world_s} "
-                  f"({rows} rows x {W}), {nf} frames = {samples} samples in {dt:.1f} s, "
-                  f"{threads} threads",
+        "threads": threads,
+        **facts,
+        "sample": f"scene {args.scene} {W}x{H} max_depth {args.depth}: rows of stripe 0/8 ({rows} rows x {W}), "
+                  f"{nf} frames = {samples} samples in {dt:.1f} s, {threads} threads",
+        "single_thread_msamples_s": round(per_thread, 3),
+        "full_host_estimate_msamples_s": round(per_thread * facts["physical_cores"], 1)
+        if facts["physical_cores"] else None,
+        "full_host_estimate_note": "single-thread rate x physical cores (extrapolated, SMT not counted): what the "
+                                   "whole host would do without the job's cgroup CPU quota",
+        "c1": {"config": "scene 9 (Book-1 three spheres), 400x225, 64 spp, max_depth 8, full render",
+               "samples": 400 * 225 * 64, "seconds": round(c1_s, 3),
+               "msamples_s": round(400 * 225 * 64 / c1_s / 1e6, 3), "threads": threads},
     }
 
 
-def bytes_per_sample(args):
-    """Committed algorithmic bytes/sample (tools/count_bytes.py)."""
-    with open(os.path.join(REPO, "bench", "bytes_per_sample.json")) as f:
-        rec = json.load(f)[f"scene{args.scene}_depth{args.depth}"]
-    c = rec["config"]
-    if (c["width"], c["height"], c["seed"]) != (args.width, args.height, args.seed):
-        log("note: bytes_per_sample.json was counted for", c)
-    return rec["bytes_per_sample"]
+# ---------------------------------------------------------------- roofline
+def roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms):
+    """VALU-issue roofline of render_persistent (see module docstring)."""
+    def load(name):
+        try:
+            with open(os.path.join(REPO, "profiles", name)) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return {}
+    key = config_key(args, frames_per_launch)
+    rec = load("valu.json").get(key)
+    if not rec:
+        log(f"no committed VALU profile for {key} (profiles/valu.json); roofline omitted")
+        return None
+    # the committed count is for rec["samples_per_launch"]; scale per sample if the launch differs
+    insts = rec["SQ_INSTS_VALU"] * samples_per_launch / rec["samples_per_launch"]
+    t = avg_launch_ms * 1e-3
+    achieved = insts / t / 1e9
+    peak_meas = load("r02_valu_peak.json").get("wave_inst_per_s_4waves")
+    traffic = rec.get("hbm_bytes_per_launch")
+    lane = rec.get("valu_lane_utilization")
+    out = {"bound": "valu", "achieved": round(achieved, 1), "peak": VALU_PEAK, "unit": "Gwave-inst/s",
+           "frac": round(achieved / VALU_PEAK, 4), "traffic": traffic,
+           "kernel": "render_persistent", "avg_launch_ms": round(avg_launch_ms, 3),
+           "samples_per_launch": samples_per_launch, "valu_insts_per_launch": insts,
+           "valu_lane_utilization": lane,
+           "lane_weighted_frac": round(achieved / VALU_PEAK * lane, 4) if lane else None,
+           "peak_measured_4waves_per_simd": round(peak_meas / 1e9, 1) if peak_meas else None,
+           "frac_of_measured_4wave_peak": round(achieved * 1e9 / peak_meas, 4) if peak_meas else None,
+           "dram_gbs": round(traffic / t / 1e9, 1) if traffic else None,
+           "dram_frac": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+           "profile": rec.get("source"),
+           "note": "achieved = SQ_INSTS_VALU per launch (rocprofv3 PMC, profiles/valu.json) / launch time measured "
+                   "live with HIP events; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction; "
+                   "lane_weighted_frac counts only the active lanes; traffic = DRAM bytes per launch "
+                   "(FETCH_SIZE x2 + WRITE_SIZE), far below HBM: the scene is LDS/L2-resident"}
+    return out
 
 
 def main():
@@ -157,17 +279,24 @@ def main():
         elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
     launches_per_step = math.ceil(F / 256)
+    avg_launch_ms = float(np.mean(kernel_ms)) / launches_per_step
     t_max = elapsed
+    rank_ms = [avg_launch_ms]
     if world > 1:
         on_gpu = torch.distributed.get_backend() == "nccl"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}" if on_gpu else "cpu")
+        tdev = f"cuda:{dev}" if on_gpu else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         t_max = float(t.item())
+        km = torch.tensor([avg_launch_ms], dtype=torch.float64, device=tdev)
+        parts = [torch.zeros_like(km) for _ in range(world)]
+        torch.distributed.all_gather(parts, km)
+        rank_ms = [float(p.item()) for p in parts]
 
     samples_total = args.width * args.height * F * args.steps   # all ranks together
     value = samples_total / t_max / 1e6
 
-    # RCCL gather of the accumulated stripes (reported separately, not in value)
+    # RCCL gather of the accumulated stripes to rank 0 (reported separately, not in value)
     torch.cuda.synchronize()
     tg = time.perf_counter()
     full = rdist.gather_image(image, args.height, world, args.stripe_rows)
@@ -190,37 +319,13 @@ def main():
             cpu = cpu_baseline(scene, args)
         except Exception as e:  # the baseline is reported, not required
             log("cpu baseline failed:", repr(e))
-    try:
-        bps = bytes_per_sample(args)
-    except (OSError, KeyError) as e:
-        log("no committed bytes/sample for this config:", repr(e))
-        bps = None
 
-    avg_launch_ms = float(np.mean(kernel_ms)) / launches_per_step
-    samples_per_launch = n_local_px * min(F, 256)
-    roofline = None
-    if bps is not None:
-        achieved = bps * samples_per_launch / (avg_launch_ms * 1e-3) / 1e9
-        traffic = None
-        try:
-            with open(os.path.join(REPO, "profiles", "traffic.json")) as f:
-                tj = json.load(f)
-            key = f"scene{args.scene}_{args.width}x{args.height}_f{min(F, 256)}_d{args.depth}"
-            traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            pass
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "bytes_per_sample": round(bps, 1), "kernel": "render_persistent",
-                    "avg_launch_ms": round(avg_launch_ms, 3), "samples_per_launch": samples_per_launch,
-                    "dram_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
-                    "note": "achieved = the reference's logical record bytes (SURVEY 8d) per launch / launch time; "
-                            "the scene is LDS/L2-resident, so frac > 1 means not HBM-bound (dram_gbs = measured "
-                            "DRAM traffic rate); the limiter is VALU issue under divergence (12% of lanes active) at 4 waves/SIMD "
-                            "(DESIGN.md section 4, profiles/r01_region_stats_v0.log)"}
+    frames_per_launch = min(F, 256)
+    samples_per_launch = n_local_px * frames_per_launch
+    roof = roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms)
 
     out = {
-        "metric": "Msamples/sec (W×H×spp/s) on Book-2 final scene @1080p, 1/2/4/8 GPUs",
+        "metric": METRIC,
         "value": round(value, 2),
         "unit": "Msamples/s",
         "n_gpus": world,
@@ -232,14 +337,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic: seeded scene {args.scene} (seed={args.seed}), built in-process",
-        "config": {"workload": f"scene{args.scene} Book-2 final, {args.width}x{args.height}, "
+        "config": {"workload": f"{args.workload_name}, {args.width}x{args.height}, sqrt_spp for {args.spp_total} spp, "
                                f"{args.frames_per_step} spp/step/rank, max_depth {args.depth}",
-                   "scene": args.scene, "width": args.width, "height": args.height,
-                   "spp_per_step": F, "max_depth": args.depth, "stripe_rows": args.stripe_rows,
-                   "parallelism": f"row-stripes x{world}"},
+                   "preset": args.preset, "scene": args.scene, "width": args.width, "height": args.height,
+                   "spp_total": args.spp_total, "spp_per_step": F, "max_depth": args.depth,
+                   "stripe_rows": args.stripe_rows, "parallelism": f"row-stripes x{world}"},
+        "kernel_ms_per_launch": {"max": round(max(rank_ms), 3), "min": round(min(rank_ms), 3)},
         "gather_ms": round(gather_ms, 3),
         "nan_pixels": nan_px,
-        "roofline": roofline,
+        "roofline": roof,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

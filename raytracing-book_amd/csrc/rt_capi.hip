@@ -40,14 +40,12 @@ struct Device {
     DevBuf image;            // internal image
     DevBuf args;             // rt_kernel_args slot in device memory
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
-    DevBuf counter;          // persistent-kernel work-unit counter
-    DevBuf samples;          // chunked launches: per-frame colours
-    DevBuf wf_q[2], wf_hits, wf_ctr;   // wavefront pipeline (variant 50)
-    DevBuf fnodes, finfo;    // exact near-first walk tables (variants 60, 61)
+    DevBuf counter;          // persistent-kernel work-unit counter [0] and fault word [1]
+    DevBuf tile_done;        // ordered chunks: chunks published per 8x8 tile
+    DevBuf finfo;            // exact near-first walk tables (variant 61)
     DevBuf f2inner, f2leaves;
-    DevBuf links;            // link-format BVH (variant 37)
+    DevBuf links;            // link-format BVH (variant 0/37)
     int fast_gen = -1;       // rt_ctx::fast_gen these copies belong to
-    unsigned* wf_host_ctr = nullptr;   // pinned readback of the queue counts
     static constexpr int kRing = 8;
     rt_kernel_args* ring = nullptr;   // pinned host staging slots for async arg uploads
     hipEvent_t ring_ev[kRing] = {};
@@ -96,21 +94,18 @@ struct rt_ctx {
     FastTables fast;
     std::vector<float4> links;   // build_links(dnodes), empty when unavailable
     int fast_gen = 0;
-    bool spec_ok = false;   // every child box lies inside its parent's (speculative walk allowed)
-    int shade_k = 32;       // decoupled schedule threshold (env RT_SHADE_K)
+    bool spec_ok = false;   // every child box lies inside its parent's (the near-first walk needs it)
     int debug_flags = 0;    // env RT_DEBUG_FLAGS: ablation runs only (bit 0: Perlin -> 0.5)
-    int wf_slots = 4 << 20; // wavefront: in-flight paths (env RT_WF_SLOTS)
-    int wf_refill = 16;     // wavefront: refill a wave once this many lanes are idle (env RT_WF_REFILL)
     bool uv_always = false;
     bool boxes_canon = false;   // every box has Box.java's axis-aligned face layout (dboxes[18..20])
     bool validated = false;
     uint64_t last_ns = 0;
     int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
+    int variant_no_stats = -1;   // the variant active before rt_debug_enable_stats(c, 1), restored by (c, 0)
     // Work split: aim for chunk_target work units per resident wave (env
-    // RT_CHUNK_TARGET; 0 = one chunk = direct mode).  Chunked launches stage
-    // per-frame colours in a device buffer of at most sample_budget bytes.
+    // RT_CHUNK_TARGET; 0 = one chunk per tile).  A launch over few tiles per wave
+    // splits its frames into ordered chunks (rt_kernel.hip wait_chunk).
     int chunk_target = 32;
-    size_t sample_budget = (size_t)4 << 30;
 };
 
 namespace {
@@ -703,12 +698,13 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (n_devices <= 0 || n_devices > 64 || (!device_ids && n_devices > count))
         return fail(RT_ERR_INVALID_ARG, "rt_create: bad device count");
     rt_ctx* c = new rt_ctx();
-    if (const char* v = std::getenv("RT_KERNEL_VARIANT")) c->variant = std::atoi(v);
+    if (const char* v = std::getenv("RT_KERNEL_VARIANT")) {
+        // 0 = 37 (default), 30, 61 and their stats twins 38, 31, 69; anything else is the default
+        const int want = std::atoi(v);
+        c->variant = (want == 30 || want == 31 || want == 37 || want == 38 || want == 61 || want == 69) ? want : 0;
+    }
     if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
-    if (const char* v = std::getenv("RT_SHADE_K")) c->shade_k = std::atoi(v);
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
-    if (const char* v = std::getenv("RT_WF_SLOTS")) c->wf_slots = std::max(256, std::atoi(v));
-    if (const char* v = std::getenv("RT_WF_REFILL")) c->wf_refill = std::min(64, std::max(1, std::atoi(v)));
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
         Device& d = c->devs[i];
@@ -733,11 +729,9 @@ int rt_destroy(rt_ctx* c) {
         (void)hipSetDevice(d.id);
         (void)hipStreamSynchronize(d.stream);
         dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
-        dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter); dev_free(d.samples);
-        dev_free(d.dquads); dev_free(d.dboxes);
-        dev_free(d.wf_q[0]); dev_free(d.wf_q[1]); dev_free(d.wf_hits); dev_free(d.wf_ctr);
-        dev_free(d.fnodes); dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links);
-        if (d.wf_host_ctr) (void)hipHostFree(d.wf_host_ctr);
+        dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter);
+        dev_free(d.tile_done); dev_free(d.dquads); dev_free(d.dboxes);
+        dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
             if (e) (void)hipEventDestroy(e);
@@ -761,23 +755,28 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
     if (nbytes % rec[binding]) return set_err(c, RT_ERR_INVALID_ARG, "size is not a multiple of the std430 record size");
     if (binding != RT_BIND_LIGHTS && nbytes / rec[binding] > RT_MAX_RECORDS)
         return set_err(c, RT_ERR_LIMIT, "more than 65535 records");
+    if (binding == RT_BIND_LIGHTS && nbytes < 4) return set_err(c, RT_ERR_INVALID_ARG, "lights buffer needs the count word");
+    std::vector<uint8_t> dev_bytes;
+    const void* src = bytes;
+    size_t n = nbytes;
+    // Thread the incoming BVH before anything of the context changes: a rejected
+    // BVH leaves the previous one (host copy, threaded nodes, device buffers) intact.
+    std::vector<rt_dnode> dn;
+    if (binding == RT_BIND_BVH) {
+        int r = thread_bvh(c, (const rt_bvh_node*)bytes, (int)(nbytes / sizeof(rt_bvh_node)), dn);
+        if (r) return r;
+        dev_bytes.assign((uint8_t*)dn.data(), (uint8_t*)dn.data() + dn.size() * sizeof(rt_dnode));
+        src = dev_bytes.data();
+        n = dev_bytes.size();
+    }
     std::vector<uint8_t>& H = c->host_buf[binding];
     H.assign((const uint8_t*)bytes, (const uint8_t*)bytes + nbytes);
     c->uploaded[binding] = true;
     c->validated = false;
-    std::vector<uint8_t> dev_bytes;
-    const void* src = bytes;
-    size_t n = nbytes;
     if (binding == RT_BIND_BVH) {
-        std::vector<rt_dnode> dn;
-        int r = thread_bvh(c, (const rt_bvh_node*)H.data(), (int)(nbytes / sizeof(rt_bvh_node)), dn);
-        if (r) return r;
         c->n_dnodes = (int)dn.size();
         c->spec_ok = boxes_nest(dn);
-        c->dnodes = dn;
-        dev_bytes.assign((uint8_t*)dn.data(), (uint8_t*)dn.data() + dn.size() * sizeof(rt_dnode));
-        src = dev_bytes.data();
-        n = dev_bytes.size();
+        c->dnodes.swap(dn);
     }
     std::vector<float4> faces;   // intersection-only copy of quads / box sides
     if (binding == RT_BIND_QUADS || binding == RT_BIND_BOXES) {
@@ -813,7 +812,6 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
             }        }
     }
     if (binding == RT_BIND_LIGHTS) {
-        if (nbytes < 4) return set_err(c, RT_ERR_INVALID_ARG, "lights buffer needs the count word");
         src = (const uint8_t*)bytes + 4;
         n = nbytes - 4;
     }
@@ -969,10 +967,8 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.uv_always = c->uv_always;
     a.boxes_canon = c->boxes_canon ? 1 : 0;
     a.variant = c->variant;
-    a.spec_ok = c->spec_ok ? 1 : 0;
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
-    a.n_fnodes = F.n_per;
     a.n_f2inner = (int)(F.inner2.size() / 4);
     a.n_f2leaves = (int)F.leaves2.size();
     a.f2depth = F.depth;
@@ -985,15 +981,15 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.fl_n = F.fl_n;
     std::memcpy(a.fl_medium, F.fl_medium, sizeof(a.fl_medium));
     std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
-    a.shade_k = c->shade_k;
     a.debug_flags = c->debug_flags;
     a.n_lnode_f4 = (int)c->links.size();
     // Perlin table in LDS after the nodes (default launch shapes only; rt_kernel.hip texture_color);
     // variant 37 stages the link-format nodes (and may use 80 KB)
-    const bool links = (c->variant == 0 || c->variant == 37 || c->variant == 38) && a.n_lnode_f4 > 0;
-    const bool shape_p = c->variant == 0 || c->variant == 30 || c->variant == 35 || c->variant == 37 || c->variant == 38;
+    const bool fast_walk = c->variant == 61 || c->variant == 69;
+    const bool links = !fast_walk && c->variant != 30 && c->variant != 31 && a.n_lnode_f4 > 0;
+    const bool shape_p = !fast_walk;
     const size_t node_f4 = links ? (size_t)a.n_lnode_f4 : (size_t)2 * c->n_dnodes;
-    const size_t lds_cap = links ? RT_LDS_FAST_BYTES : RT_LDS_NODE_BYTES;
+    const size_t lds_cap = links ? RT_LDS_DYN_BYTES : RT_LDS_NODE_BYTES;
     a.perlin_slot = a.perlin_lds = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
@@ -1008,31 +1004,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                             (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] / 4 : 0);
         if (a.n_media > 0 && a.n_media <= 64 && shape_p && (base + 3 * (size_t)a.n_media) * 16 <= lds_cap)
             a.media_lds = (int)base;
-    }
-    // variant 36 (one 1024-thread workgroup per CU, all 160 KB of LDS): also the spheres'
-    // intersection data and the canonical box planes
-    a.n_spheres = (int)(c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere));
-    a.n_boxes = (int)(c->host_buf[RT_BIND_BOXES].size() / sizeof(rt_box));
-    a.sph_lds = a.boxc_lds = -1;
-    if (c->variant == 36) {
-        a.perlin_lds = -1;
-        a.media_lds = -1;
-        size_t off = (size_t)2 * c->n_dnodes;
-        if (a.perlin_slot >= 0) {
-            a.perlin_lds = (int)off;
-            off += ((size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] + 3) / 4;
-        }
-        if (a.n_media > 0 && a.n_media <= 64) {
-            a.media_lds = (int)off;
-            off += 3 * (size_t)a.n_media;
-        }
-        a.sph_lds = (int)off;
-        off += 2 * (size_t)a.n_spheres;
-        if (c->boxes_canon) {
-            a.boxc_lds = (int)off;
-            off += 3 * (size_t)a.n_boxes;
-        }
-        if (off * 16 > RT_LDS_CU_BYTES) a.perlin_lds = a.media_lds = a.sph_lds = a.boxc_lds = -1;
     }
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
@@ -1067,6 +1038,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         if (!d.args.ptr) {
             HIPCHK(c, hipMalloc(&d.counter.ptr, 256));
             d.counter.bytes = 256;
+            HIPCHK(c, hipMemsetAsync(d.counter.ptr, 0, 256, d.stream));
             HIPCHK(c, hipMalloc(&d.args.ptr, sizeof(rt_kernel_args)));
             d.args.bytes = sizeof(rt_kernel_args);
             HIPCHK(c, hipHostMalloc((void**)&d.ring, sizeof(rt_kernel_args) * Device::kRing, hipHostMallocDefault));
@@ -1074,73 +1046,36 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         }
         a.tile_counter = (int*)d.counter.ptr;
         if (d.fast_gen != c->fast_gen) {
-            int rf = dev_alloc_copy(c, d, d.fnodes, F.nodes.data(), F.nodes.size() * sizeof(rt_dnode));
-            if (!rf) rf = dev_alloc_copy(c, d, d.finfo, F.info.data(), F.info.size() * sizeof(uint32_t));
+            int rf = dev_alloc_copy(c, d, d.finfo, F.info.data(), F.info.size() * sizeof(uint32_t));
             if (!rf) rf = dev_alloc_copy(c, d, d.f2inner, F.inner2.data(), F.inner2.size() * sizeof(float4));
             if (!rf) rf = dev_alloc_copy(c, d, d.f2leaves, F.leaves2.data(), F.leaves2.size() * sizeof(uint2));
             if (!rf) rf = dev_alloc_copy(c, d, d.links, c->links.data(), c->links.size() * sizeof(float4));
             if (rf) return rf;
             d.fast_gen = c->fast_gen;
         }
-        a.fnodes = (const float4*)d.fnodes.ptr;
         a.finfo = (const uint32_t*)d.finfo.ptr;
         a.f2inner = (const float4*)d.f2inner.ptr;
         a.f2leaves = (const uint2*)d.f2leaves.ptr;
         a.lnodes = (const float4*)d.links.ptr;
-        a.n_pixels = (size_t)d.local_rows * c->width;
         // Frames per launch and the unit split.  Units = tiles x chunks; with too
         // few tiles per resident wave (small images, N-GPU stripes) the frames
-        // are chunked so the dynamic schedule has enough units to balance.
+        // are split into ordered chunks so the dynamic schedule has enough units
+        // to balance (rt_kernel.hip wait_chunk / publish_chunk).
         const int n_tiles = ((c->width + 7) / 8) * ((d.local_rows + 7) / 8);
-        int per_launch = RT_MAX_FRAMES_PER_LAUNCH;
+        const int per_launch = RT_MAX_FRAMES_PER_LAUNCH;
         int chunks_wanted = 1;
         if (c->chunk_target > 0 && n_tiles > 0) {
             long long waves = rt_resident_waves();
             chunks_wanted = (int)std::min<long long>(RT_MAX_FRAMES_PER_LAUNCH,
                                                      (c->chunk_target * waves + n_tiles - 1) / n_tiles);
         }
-        const bool wavefront = c->variant == 50;
-        if (wavefront) chunks_wanted = std::max(chunks_wanted, 2);   // always stages per-frame colours
-        if (chunks_wanted > 1) {
-            size_t per_frame = a.n_pixels * sizeof(float4);
-            per_launch = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, c->sample_budget / per_frame));
-            size_t need = per_frame * (size_t)std::min(per_launch, n_frames);
-            if (d.samples.bytes < need) {
-                dev_free(d.samples);
-                HIPCHK(c, hipMalloc(&d.samples.ptr, need));
-                d.samples.bytes = need;
-            }
+        if (chunks_wanted > 1 && d.tile_done.bytes < sizeof(unsigned) * (size_t)n_tiles) {
+            dev_free(d.tile_done);
+            HIPCHK(c, hipMalloc(&d.tile_done.ptr, sizeof(unsigned) * (size_t)n_tiles));
+            d.tile_done.bytes = sizeof(unsigned) * (size_t)n_tiles;
         }
-        a.wf_tiles = n_tiles;
-        a.wf_refill = c->wf_refill;
-        if (wavefront) {
-            // in-flight path slots: enough queued rays to keep every lane walking
-            size_t total = (size_t)n_tiles * 64 * (size_t)std::min(per_launch, std::max(n_frames, 1));
-            int slots = (int)std::min<size_t>((size_t)c->wf_slots, std::max<size_t>(total, 1));
-            if (!d.wf_ctr.ptr) {
-                HIPCHK(c, hipMalloc(&d.wf_ctr.ptr, 64));
-                d.wf_ctr.bytes = 64;
-                HIPCHK(c, hipHostMalloc((void**)&d.wf_host_ctr, 64, hipHostMallocDefault));
-            }
-            size_t qb = (size_t)slots * WF_REC_F4 * sizeof(float4), hb = (size_t)slots * WF_HIT_F4 * sizeof(float4);
-            for (int k = 0; k < 2; k++)
-                if (d.wf_q[k].bytes < qb) {
-                    dev_free(d.wf_q[k]);
-                    HIPCHK(c, hipMalloc(&d.wf_q[k].ptr, qb));
-                    d.wf_q[k].bytes = qb;
-                }
-            if (d.wf_hits.bytes < hb) {
-                dev_free(d.wf_hits);
-                HIPCHK(c, hipMalloc(&d.wf_hits.ptr, hb));
-                d.wf_hits.bytes = hb;
-            }
-            a.wf_slots = slots;
-            a.wf_q[0] = (float4*)d.wf_q[0].ptr;
-            a.wf_q[1] = (float4*)d.wf_q[1].ptr;
-            a.wf_hits = (float4*)d.wf_hits.ptr;
-            a.wf_ctr = (unsigned*)d.wf_ctr.ptr;
-            a.wf_next = (unsigned long long*)((char*)d.wf_ctr.ptr + 32);
-        }
+        a.tile_done = (unsigned*)d.tile_done.ptr;
+        a.fault = (unsigned*)d.counter.ptr + 1;
         HIPCHK(c, hipEventRecord(d.ev_start, d.stream));
         for (int f0 = 0; f0 < n_frames; f0 += per_launch) {
             int nf = std::min(per_launch, n_frames - f0);
@@ -1149,13 +1084,11 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             a.n_chunks = std::max(1, std::min(chunks_wanted, nf));
             a.chunk_frames = (nf + a.n_chunks - 1) / a.n_chunks;
             a.n_chunks = (nf + a.chunk_frames - 1) / a.chunk_frames;
-            a.samples = (a.n_chunks > 1 || wavefront) ? (float4*)d.samples.ptr : nullptr;
-            a.wf_total = (unsigned long long)n_tiles * 64ull * (unsigned long long)nf;
             std::memcpy(a.rand_factors, rand_factors + f0, sizeof(float) * nf);
             int slot = d.ring_pos++ % Device::kRing;
             HIPCHK(c, hipEventSynchronize(d.ring_ev[slot]));   // the copy that last used this slot is done
             d.ring[slot] = a;
-            if (rt_launch_render(d.ring[slot], (rt_kernel_args*)d.args.ptr, d.stream, d.wf_host_ctr))
+            if (rt_launch_render(d.ring[slot], (rt_kernel_args*)d.args.ptr, d.stream))
                 return set_err(c, RT_ERR_DEVICE, std::string("kernel launch failed: ") +
                                                      hipGetErrorString(hipGetLastError()));
             HIPCHK(c, hipEventRecord(d.ring_ev[slot], d.stream));
@@ -1172,6 +1105,14 @@ int rt_sync(rt_ctx* c) {
     for (Device& d : c->devs) {
         HIPCHK(c, hipSetDevice(d.id));
         HIPCHK(c, hipStreamSynchronize(d.stream));
+        if (d.counter.ptr) {   // fault word: an ordered-chunk wait timed out (never expected)
+            unsigned fault = 0;
+            HIPCHK(c, hipMemcpy(&fault, (unsigned*)d.counter.ptr + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+            if (fault) {
+                HIPCHK(c, hipMemset((unsigned*)d.counter.ptr + 1, 0, sizeof(unsigned)));
+                return set_err(c, RT_ERR_DEVICE, "render kernel: ordered-chunk wait timed out");
+            }
+        }
     }
     return RT_OK;
 }
@@ -1344,6 +1285,13 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
     return (F.ok && boxes_nest(dn)) ? 1 : 0;
 }
 
+// The stats twin (region timers + lane counters) of a launch variant: 61 -> 69, 30 -> 31, 0/37 -> 38.
+static int stats_twin(int v) {
+    if (v == 61 || v == 69) return 69;
+    if (v == 30 || v == 31) return 31;
+    return 38;
+}
+
 int rt_debug_enable_stats(rt_ctx* c, int on) {
     if (!c) return RT_ERR_INVALID_ARG;
     for (Device& d : c->devs) {
@@ -1358,10 +1306,11 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
     }
     // stats twin of the current launch shape: 12/15/30 -> 31, 10 -> 19, 0/37 -> 38
     if (on) {
-        int v = c->variant;
-        c->variant = (v == 10 || v == 19) ? 19 : (v >= 40 && v < 50) ? 49 : (v == 60 || v == 68) ? 68 : (v == 61 || v == 69) ? 69 : (v == 0 || v == 37 || v == 38) ? 38 : 31;
-    } else {
-        c->variant = 0;
+        if (c->variant_no_stats < 0) c->variant_no_stats = c->variant;
+        c->variant = stats_twin(c->variant_no_stats);
+    } else if (c->variant_no_stats >= 0) {
+        c->variant = c->variant_no_stats;
+        c->variant_no_stats = -1;
     }
     return RT_OK;
 }

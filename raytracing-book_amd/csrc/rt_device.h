@@ -14,7 +14,7 @@
 //   lights   : int32 packed ids
 //   textures : RGB8 expanded to RGBA8 (4 B/texel, aligned), RGBA8, R32F
 //   image    : float4 [padded_local_rows][W], stripe-compacted rows
-//   samples  : float4 [frames][local_rows*W] per-frame colours (chunked launches only)
+//   tile_done: uint32 [tiles] chunks published per 8x8 tile (ordered-chunk launches)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -26,11 +26,11 @@
 #define RT_NODE_END 0xFFFFu
 #define RT_DFACE_F4 3    // float4 per dquads record
 #define RT_DBOX_F4 21    // float4 per dboxes record
-#define WF_REC_F4 5      // wavefront queue record (path state), float4
-#define WF_HIT_F4 2      // wavefront hit record, float4
-#define RT_LDS_NODE_BYTES (64 * 1024)   // stage the BVH in LDS when it fits (2 workgroups/CU)
-#define RT_LDS_FAST_BYTES (80 * 1024)   // variant 61: two-child tree + stacks in LDS (2 workgroups/CU)
-#define RT_LDS_CU_BYTES (160 * 1024)    // variant 36: one workgroup per CU takes all of it
+// LDS per 512-thread workgroup (2 workgroups per CU share 160 KiB): the static
+// running-mean slots (RT_LDS_ACC_BYTES) + the dynamic region (RT_LDS_DYN_BYTES)
+#define RT_LDS_ACC_BYTES (512 * 16)
+#define RT_LDS_DYN_BYTES (80 * 1024 - RT_LDS_ACC_BYTES)   // link nodes + Perlin + media, or variant 61's tree + stacks
+#define RT_LDS_NODE_BYTES (64 * 1024)   // threaded (meta-word) nodes in LDS when they fit
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
 // continues at index+1 (its RIGHT child, which the reference visits first
@@ -86,43 +86,31 @@ struct rt_kernel_args {
     int first_frame, n_frames;
     unsigned long long* stats;   // diagnostic counters (stats variant only)
     int* tile_counter;           // persistent kernel: next work unit (zeroed per launch)
-    // work split: unit = chunk * n_tiles + tile, chunk = frames [c*chunk_frames, ...)
+    // work split: unit = chunk * n_tiles + tile, chunk = frames [c*chunk_frames, ...) (ordered chunks)
     int n_chunks, chunk_frames;
-    float4* samples;             // chunked mode: per-frame colours [n_frames][n_pixels]; nullptr = direct
-    size_t n_pixels;             // local_rows * width
-    int shade_k;                 // decoupled schedule: shade once this many lanes wait
-    // wavefront pipeline (variant 50): two path queues, hit records, counters
-    float4* wf_q[2];             // [wf_slots][WF_REC_F4]
-    float4* wf_hits;             // [wf_slots][WF_HIT_F4], by queue position
-    unsigned* wf_ctr;            // [0],[1] queue counts, [2] trace fetch head
-    unsigned long long* wf_next; // next unstarted path id
-    unsigned long long wf_total; // path ids: wf_tiles * 64 * n_frames
-    int wf_slots, wf_tiles, wf_refill;
+    unsigned* tile_done;         // ordered chunks: per tile, the chunks published so far (zeroed per launch)
+    unsigned* fault;             // set when an ordered-chunk wait times out (rt_sync reports it)
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
     int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1
     int perlin_lds;              // its float4 offset in the dynamic LDS (after the nodes), or -1
-    int n_media, n_spheres, n_boxes;
-    int sph_lds, boxc_lds;       // variant 36: float4 offsets in LDS of the spheres' first two float4 and the
-                                 // boxes' canonical plane tails (3 float4), or -1
+    int n_media;
     int media_lds;               // float4 offset of the media records + sphere boundaries in LDS (3 float4
                                  // per medium, after the Perlin table), or -1
-    int spec_ok;                 // BVH boxes nest (child inside parent): speculative walk allowed
-    // exact near-first walk (variant 60; tables from rt_capi.hip build_fast)
-    const float4* fnodes;        // 8 octant layouts x n_fnodes threaded SAH nodes (rt_dnode), near child first
+    // exact near-first walk (variant 61; tables from rt_capi.hip build_fast)
     const uint32_t* finfo;       // per solid prim (finfo_base[type] + index): reference rank << 16 | reference leaf
-    int n_fnodes, fast_ok;
+    int fast_ok;
     int finfo_base[8];
     int fm_n;                    // media slots in the reference's visit order
     int fm_medium[4], fm_leaf[4], fm_track[4], fm_flags[4];   // flags: 1 same leaf as the previous slot, 2 solid first
     int fl_n;                    // trackers: the closest solid ranked before a constrained media slot
     int fl_medium[2], fl_rank[2];
-    // the same tree as two-child nodes for the stack walk (variant 61; FastTables::inner2/leaves2)
+    // the SAH tree as two-child nodes for the stack walk (FastTables::inner2/leaves2)
     const float4* f2inner;       // 4 float4 per inner node: left box, right box, refs + tracker bits
     const uint2* f2leaves;       // (meta, prims) per leaf
     int n_f2inner, n_f2leaves, f2depth;
-    // the reference's threaded BVH with explicit successors (variant 37; rt_capi.hip build_links)
+    // the reference's threaded BVH with explicit successors (variant 0/37; rt_capi.hip build_links)
     const float4* lnodes;        // 2 float4 per node, then the leaves' (types, prims) as uint2
     int n_lnode_f4;              // float4 of the whole array; 0 = not available (too many nodes)
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
@@ -130,6 +118,6 @@ struct rt_kernel_args {
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves the default launch shape keeps resident on the current device
-int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream, unsigned* host_ctr);
+int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream);
 // debug: evaluate GLSL built-ins on device (tests)
 int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream);

@@ -383,7 +383,7 @@ __device__ __forceinline__ bool aabb_pk(float4 n0, float4 n1, v3 o, v3 inv, floa
 }
 
 // The two prims of a leaf (compute.glsl:247-256), left then right.
-template <bool STATS, bool LP = false>
+template <bool STATS>
 __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a, float time,
                                            float tmin, float& tmax, float& rf, float px, float py, Hit& h, bool& has,
                                            unsigned long long* st) {
@@ -404,17 +404,14 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
         int face = 0;
         bool hit = false;
         if (ty == RT_MODEL_SPHERE) {
-            hit = sphere_t(LP ? rt_dyn_lds + P.sph_lds + 2 * ix : reinterpret_cast<const float4*>(P.spheres + ix), time,
-                           o, d, a, tmin, tmax, t);
+            hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t);
             if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
         } else if (ty == RT_MODEL_QUAD) {
             hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, tmax, t, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_BOX) {
-            hit = (P.boxes_canon && fin)
-                      ? box_test_canon((LP && P.boxc_lds >= 0) ? rt_dyn_lds + P.boxc_lds + 3 * ix
-                                                               : P.dboxes + RT_DBOX_F4 * ix + 18,
-                                       P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be)
+            hit = (P.boxes_canon && fin) ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix + 18, P.dboxes + RT_DBOX_F4 * ix, o,
+                                                          d, tmin, tmax, t, face, al, be)
                                          : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
@@ -431,9 +428,10 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
 // compute.glsl:226-266 over the threaded BVH.  Each lane's node sequence is the
 // reference's; only the interleaving of a wave's lanes differs: lanes advance
 // through inner/missed nodes until each holds a hit leaf (or is done), then the
-// leaves are tested together ("while-while").  WHILE_WHILE bit 1 selects the
-// branch-free node step with the NaN-exact min/max slab test.
-template <int WHILE_WHILE, bool STATS, bool LP = false>
+// leaves are tested together ("while-while").  LINK (variant 0/37): link-format
+// nodes; otherwise (variant 30) the threaded nodes with their meta word.  Both
+// use the branch-free node step with the NaN-exact min/max slab test.
+template <bool LINK, bool STATS>
 __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ nodes, v3 o, v3 d, float time,
                                       float& rf, float px, float py, Hit& h, unsigned long long* st) {
     if (P.n_nodes == 0) return false;
@@ -444,8 +442,8 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
     uint32_t i = 0;
     // rays that need the exact slab (see aabb_fast); wave-uniform fast path otherwise
     const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
-    const bool wave_exact = (WHILE_WHILE & 2) ? (__ballot(lane_exact) != 0) : true;   // uniform
-    if (WHILE_WHILE & 8) {
+    const bool wave_exact = __ballot(lane_exact) != 0;   // uniform
+    if (LINK) {
         // link-format nodes (rt_device.h RT_LINK_*): the successor is one select
         // between the node's hit and miss words; a hit leaf or the end leaves
         // the loop (sign bit)
@@ -475,108 +473,48 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
             unsigned long long t1 = STATS ? clock64() : 0;
             if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
             const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
-            leaf_prims<STATS, LP>(P, lf.x, lf.y, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            leaf_prims<STATS>(P, lf.x, lf.y, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
             if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
             nx &= 0xFFFFu;
             if (nx == 0xFFFFu) break;
         }
         return has;
     }
-    if (WHILE_WHILE & 2) {
-        // while-while with a branch-free node step and one loop exit: a hit inner
-        // node continues at i+1 (its right child), anything else at the skip
-        // link; a hit leaf leaves the loop with its prims pending.
-        for (;;) {
-            uint32_t meta = 0, prims = 0;
-            bool leaf = false;
-            unsigned long long t0 = STATS ? clock64() : 0;
-            if (i != RT_NODE_END && (WHILE_WHILE & 4)) {
-                // software-pipelined: both possible successors (i+1 and the skip
-                // link) are fetched while node i is tested
-                const uint32_t last = (uint32_t)P.n_nodes - 1;
-                float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
-                for (;;) {
-                    if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-                    meta = __float_as_uint(n1.z);
-                    prims = __float_as_uint(n1.w);
-                    const uint32_t skip = meta & 0xFFFFu;
-                    const uint32_t j1 = min(i + 1, last), j2 = (skip == RT_NODE_END) ? 0u : skip;
-                    float4 b0 = nodes[2 * j1], b1 = nodes[2 * j1 + 1];
-                    float4 c0 = nodes[2 * j2], c1 = nodes[2 * j2 + 1];
-                    bool hitn;
-                    if (!wave_exact) {
-                        hitn = aabb_fast(n0, n1, o, inv, tmin, tmax);
-                    } else {
-                        float lo = tmin, hi = tmax;
-                        slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-                        slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-                        slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-                        hitn = !(hi <= lo);
-                    }
-                    bool inner = (meta & 0xF0000u) == 0;
-                    bool down = hitn && inner;
-                    i = down ? i + 1 : skip;
-                    leaf = hitn && !inner;
-                    if (leaf || i == RT_NODE_END) break;
-                    n0 = down ? b0 : c0;
-                    n1 = down ? b1 : c1;
-                }
-            } else if (i != RT_NODE_END) {
-                for (;;) {
-                    if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-                    float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
-                    meta = __float_as_uint(n1.z);
-                    prims = __float_as_uint(n1.w);
-                    bool hitn;
-                    if (!wave_exact) {
-                        hitn = aabb_fast(n0, n1, o, inv, tmin, tmax);
-                    } else {
-                        float lo = tmin, hi = tmax;
-                        slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-                        slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-                        slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-                        hitn = !(hi <= lo);
-                    }
-                    bool inner = (meta & 0xF0000u) == 0;
-                    i = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
-                    leaf = hitn && !inner;
-                    if (leaf || i == RT_NODE_END) break;
-                }
-            }
-            if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
-            if (!leaf) break;
-            unsigned long long t1 = STATS ? clock64() : 0;
-            if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-            leaf_prims<STATS, LP>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
-            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-        }
-    } else {
-        for (;;) {
-            uint32_t meta = 0, prims = 0;
-            bool leaf = false;
-            unsigned long long t0 = STATS ? clock64() : 0;
-            while (i != RT_NODE_END) {
+    // threaded nodes with the meta word: a hit inner node continues at i+1 (its
+    // right child), anything else at the skip link; a hit leaf leaves the loop
+    // with its prims pending.
+    for (;;) {
+        uint32_t meta = 0, prims = 0;
+        bool leaf = false;
+        unsigned long long t0 = STATS ? clock64() : 0;
+        if (i != RT_NODE_END) {
+            for (;;) {
                 if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
                 float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
                 meta = __float_as_uint(n1.z);
                 prims = __float_as_uint(n1.w);
-                float lo = tmin, hi = tmax;
-                slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-                slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-                slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-                if (hi <= lo) { i = meta & 0xFFFFu; continue; }
-                if (((meta >> 16) & 0xFu) == 0) { i = i + 1; continue; }
-                leaf = true;
-                break;
+                bool hitn;
+                if (!wave_exact) {
+                    hitn = aabb_fast(n0, n1, o, inv, tmin, tmax);
+                } else {
+                    float lo = tmin, hi = tmax;
+                    slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+                    slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+                    slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+                    hitn = !(hi <= lo);
+                }
+                bool inner = (meta & 0xF0000u) == 0;
+                i = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
+                leaf = hitn && !inner;
+                if (leaf || i == RT_NODE_END) break;
             }
-            if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
-            if (!leaf) break;
-            unsigned long long t1 = STATS ? clock64() : 0;
-            if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-            leaf_prims<STATS, LP>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
-            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-            i = meta & 0xFFFFu;
         }
+        if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
+        if (!leaf) break;
+        unsigned long long t1 = STATS ? clock64() : 0;
+        if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+        leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+        if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
     }
     return has;
 }
@@ -836,7 +774,7 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, float& rf, float 
 }
 
 // ===========================================================================
-// Exact near-first walk (variant 60).  The reference walks its own median-split
+// Exact near-first walk (variant 61).  The reference walks its own median-split
 // BVH in a fixed right-first order (compute.glsl:226-266) and keeps the LAST
 // hit it accepts.  For a ray with a finite origin and no -inf/NaN in 1/dir this walk
 // returns the same hit from a SAH tree over the BVH's solid prims, visited
@@ -895,9 +833,8 @@ __device__ __forceinline__ bool ref_leaf_hit(const float4* __restrict__ rn, uint
     return aabb_fast(rn[2 * k], rn[2 * k + 1], o, inv, 0.001f, tmax);
 }
 
-// MODE 1: threaded octant layouts (global memory); MODE 2: two-child nodes, near
-// child first by entry distance, per-lane stack (fc).
-template <int MODE, bool STATS = false>
+// Two-child nodes, near child first by entry distance, per-lane stack (fc).
+template <bool STATS = false>
 __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict__ rn, const FastCtx& fc, v3 o, v3 d,
                                           float time, float& rf, float px, float py, Hit& h, bool& has,
                                           unsigned long long* st = nullptr) {
@@ -969,37 +906,7 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
             }
         }
     };
-    if (MODE == 1) {
-        const int oct = (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
-        const float4* __restrict__ fn = P.fnodes + (size_t)oct * 2u * (size_t)P.n_fnodes;
-        uint32_t i = P.n_fnodes > 0 ? 0u : RT_NODE_END;
-        for (;;) {
-            uint32_t meta = 0, prims = 0;
-            bool leaf = false;
-            unsigned long long c0 = STATS ? clock64() : 0;
-            while (i != RT_NODE_END) {
-                if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-                n_steps++;
-                const float4 n0 = fn[2 * i], n1 = fn[2 * i + 1];
-                meta = __float_as_uint(n1.z);
-                prims = __float_as_uint(n1.w);
-                float bound = pb;
-                if (meta & (1u << 24)) bound = fmax2(bound, pb0);
-                if (meta & (1u << 25)) bound = fmax2(bound, pb1);
-                const bool hitn = aabb_fast(n0, n1, o, inv, tmin, bound);
-                const bool inner = (meta & 0xF0000u) == 0;
-                i = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
-                leaf = hitn && !inner;
-                if (leaf) break;
-            }
-            if (STATS) st_add(st, ST_NODE_CYC, clock64() - c0);
-            if (!leaf) break;
-            unsigned long long c1 = STATS ? clock64() : 0;
-            if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-            leaf_test(meta, prims);
-            if (STATS) st_add(st, ST_LEAF_CYC, clock64() - c1);
-        }
-    } else {
+    {
         constexpr int EMPTY = -0x40000000;   // refs are 16-bit: never a node
         int n = P.n_f2inner > 0 ? 0 : (P.n_f2leaves > 0 ? ~0 : EMPTY);
         int sp = 0;
@@ -1254,7 +1161,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 }
 
 // One iteration of ray_color's loop (compute.glsl:304-340).
-template <int WW, bool STATS, int FAST = 0, bool LP = false>
+template <bool LINK, bool STATS, bool FAST>
 __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, Path& S,
                                        float px, float py, v3& result, unsigned long long* st) {
     if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
@@ -1273,18 +1180,18 @@ __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ n
     } else if (FAST && P.fast_ok) {
         const float rf0 = S.rf;
         bool fh = false;
-        const int why = trace_fast<FAST, STATS>(P, nodes, fc, S.o, d, S.time, S.rf, px, py, h, fh, st);
+        const int why = trace_fast<STATS>(P, nodes, fc, S.o, d, S.time, S.rf, px, py, h, fh, st);
         if (STATS) fast_count(st, why);
         if (why == 0) {
             hit = fh;
         } else {   // the exact walk, from the same rand() state
             unsigned long long c_ex = STATS ? clock64() : 0;
             S.rf = rf0;
-            hit = trace<WW, STATS, LP>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+            hit = trace<LINK, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
             if (STATS) st_add(st, ST_FAST_EXACT_CYC, clock64() - c_ex);
         }
     } else {
-        hit = trace<WW, STATS, LP>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+        hit = trace<LINK, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
     }
     unsigned long long ts = STATS ? clock64() : 0;
     if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
@@ -1344,24 +1251,17 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
 }
 
 // compute.glsl:345-358 for frames [f0, f1) of the launch, for the pixel at
-// column x of local (stripe-compacted) row lr.  Path regeneration: a lane whose
-// path ended starts its next frame at once; each pixel still runs its frames
-// in order.  Direct mode (P.samples == nullptr): the running mean is applied
-// per frame in registers and the image is read/written once.  Chunked mode:
-// each frame's colour goes to P.samples[f][pixel] and fold_kernel applies the
-// running mean afterwards in frame order (the same operations, so the same bits).
-// SMODE: 0 = direct/chunked chosen at run time, 1 = direct only, 2 = chunked
-// only (no running-mean registers live across the frame loop).
-template <int WW, bool STATS, int SMODE = 0, int FAST = 0, bool LP = false>
+// column x of local (stripe-compacted) row lr, with the running mean
+// (compute.glsl:355) kept in the lane's LDS slot `acc` between frames (not in
+// registers: the four floats would be live across the whole bounce loop, which
+// costs spills at 128 VGPRs).  Path regeneration: a lane whose path ended
+// starts its next frame at once; each pixel still runs its frames in order, and
+// the mean is applied per frame in the reference's order.
+template <bool LINK, bool STATS, bool FAST>
 __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, int x,
-                                             int lr, int f0, int f1, unsigned long long* st) {
+                                             int lr, int f0, int f1, float4* acc, unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
     int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
-    const size_t pix = (size_t)lr * P.width + x;
-    float4* px = reinterpret_cast<float4*>(P.image) + pix;
-    const bool direct = SMODE == 1 || (SMODE == 0 && P.samples == nullptr);
-    float4 prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (direct) prev = *px;
     const rt_camera_ubo& C = P.cam;
     float fx = (float)x, fy = (float)y;
     // get_norm_coord (compute.glsl:268-283) before its jitter term: per pixel
@@ -1379,250 +1279,74 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
             fresh = false;
         }
         v3 cur;
-        if (bounce<WW, STATS, FAST, LP>(P, nodes, fc, S, fx, fy, cur, st)) {
-            if (direct) {
-                int fc = P.first_frame + f;
-                float n1 = (float)(fc - 1), n = (float)fc;
-                prev.x = (prev.x * n1 + cur.x) / n;
-                prev.y = (prev.y * n1 + cur.y) / n;
-                prev.z = (prev.z * n1 + cur.z) / n;
-                prev.w = 1.0f;
-            } else {
-                P.samples[(size_t)f * P.n_pixels + pix] = make_float4(cur.x, cur.y, cur.z, 0.0f);
-            }
+        if (bounce<LINK, STATS, FAST>(P, nodes, fc, S, fx, fy, cur, st)) {
+            int fc = P.first_frame + f;
+            float n1 = (float)(fc - 1), n = (float)fc;
+            float4 prev = *acc;
+            prev.x = (prev.x * n1 + cur.x) / n;
+            prev.y = (prev.y * n1 + cur.y) / n;
+            prev.z = (prev.z * n1 + cur.z) / n;
+            prev.w = 1.0f;
+            *acc = prev;
             f++;
             fresh = true;
         }
     }
-    if (direct) *px = prev;
 }
 
-// ---------------------------------------------------------------------------
-// Decoupled schedule (variant 40+): a lane's trace state lives across the
-// wave's stages, so lanes whose trace ended wait for shading while the others
-// keep walking, and the wave shades once >= P.shade_k lanes wait (or no lane is
-// walking).  Within a trace, lanes with finite 1/dir keep walking past a hit
-// leaf ("speculative" walk) and queue up to Q leaves; the queue is drained in
-// order, one leaf per lane per leaf stage.
-//
-// Why a walk past a pending leaf stays exact: a queued leaf's prims may shrink
-// ray_t.max, so the inner nodes tested meanwhile saw a stale (larger) max.  The
-// reference visits leaf L iff L's AABB passes at the max current when L is
-// popped (its ancestors then pass too: child boxes lie inside their parent's
-// box, AABB.java join/pad only grow, and with finite 1/dir the slab interval
-// is monotone in the box bounds and in ray_t.max).  A larger max only admits
-// more inner nodes, so the walk enumerates a superset of the reference's
-// leaves in the reference's pre-order, and every leaf's AABB is re-tested
-// exactly with the current max when it is dequeued.  Media draw rand() only in
-// the leaf stage, in that same order.  The host checks the box nesting on
-// upload (P.spec_ok); rays with an infinite 1/dir component never speculate.
-struct Trace {
-    Hit h;
-    v3 inv;
-    float a, tmax;
-    uint32_t ni;      // next node of the walk (RT_NODE_END: walk finished)
-    uint64_t q;       // queued leaf nodes, 16 bits each, head in the low bits
-    int qn;           // queue length
-    bool has;
-    bool exact;       // 1/dir has a -inf component: exact slab semantics
-    bool spec;        // may walk past a queued leaf
-};
-
-// compute.glsl:304-306 + trace_through_bvh's prologue (:226-236) for S's ray.
-// Returns false when the loop bound ends the sample (final_color stays 0).
-__device__ __forceinline__ bool begin_trace(const KP& P, Path& S, Trace& T) {
-    if (S.depth >= P.max_depth) return false;
-    S.depth++;
-    v3 d = S.d;
-    T.h.t = 0.0f; T.h.type = 0; T.h.idx = 0; T.h.face = 0;
-    T.h.uv_kind_idx = 0; T.h.uv_a = 0.0f; T.h.uv_b = 0.0f;
-    T.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    T.a = g_dot(d, d);
-    T.tmax = RT_INFINITY;
-    T.has = false;
-    T.q = 0;
-    T.qn = 0;
-    // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
-    bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
-    T.ni = (dir_zero || P.n_nodes == 0) ? RT_NODE_END : 0u;
-    T.exact = (T.inv.x == -INFINITY) || (T.inv.y == -INFINITY) || (T.inv.z == -INFINITY);
-    T.spec = P.spec_ok && fabsf(T.inv.x) < INFINITY && fabsf(T.inv.y) < INFINITY && fabsf(T.inv.z) < INFINITY;
-    return true;
-}
-
-// The node at T.ni (compute.glsl:237-262): inner hit -> its right child
-// (T.ni + 1), leaf hit -> queued, anything else -> the skip link.
-__device__ __forceinline__ void node_step(const float4* __restrict__ nodes, Trace& T, v3 o, bool wave_exact) {
-    const uint32_t i = T.ni;
-    float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
-    uint32_t meta = __float_as_uint(n1.z);
-    bool hitn;
-    if (!wave_exact) {
-        hitn = aabb_fast(n0, n1, o, T.inv, 0.001f, T.tmax);
-    } else {
-        float lo = 0.001f, hi = T.tmax;
-        slab(n0.x, n0.y, o.x, T.inv.x, lo, hi);
-        slab(n0.z, n0.w, o.y, T.inv.y, lo, hi);
-        slab(n1.x, n1.y, o.z, T.inv.z, lo, hi);
-        hitn = !(hi <= lo);
-    }
-    bool inner = (meta & 0xF0000u) == 0;
-    T.ni = (hitn && inner) ? i + 1 : (meta & 0xFFFFu);
-    if (hitn && !inner) {
-        T.q |= (uint64_t)i << (16 * T.qn);
-        T.qn++;
-    }
-}
-
-// Dequeue the head leaf, re-test its AABB with the current ray_t.max and, on a
-// hit, test its two prims (compute.glsl:247-256).
-template <bool STATS>
-__device__ __forceinline__ void leaf_stage(const KP& P, const float4* __restrict__ nodes, Path& S, Trace& T, float px,
-                                           float py, unsigned long long* st) {
-    const uint32_t i = (uint32_t)(T.q & 0xFFFFu);
-    T.q >>= 16;
-    T.qn--;
-    float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
-    bool hitn;
-    if (!T.exact) {
-        hitn = aabb_fast(n0, n1, S.o, T.inv, 0.001f, T.tmax);
-    } else {
-        float lo = 0.001f, hi = T.tmax;
-        slab(n0.x, n0.y, S.o.x, T.inv.x, lo, hi);
-        slab(n0.z, n0.w, S.o.y, T.inv.y, lo, hi);
-        slab(n1.x, n1.y, S.o.z, T.inv.z, lo, hi);
-        hitn = !(hi <= lo);
-    }
-    if (hitn)
-        leaf_prims<STATS>(P, __float_as_uint(n1.z), __float_as_uint(n1.w), S.o, S.d, T.a, S.time, 0.001f, T.tmax, S.rf,
-                          px, py, T.h, T.has, st);
-}
-
-template <int Q, bool STATS>
-__device__ __forceinline__ void render_pixel_dec(const KP& P, const float4* __restrict__ nodes, int x, int lr, int f0,
-                                                 int f1, bool valid, unsigned long long* st) {
-    int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
-    int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
-    const size_t pix = (size_t)lr * P.width + x;
-    float4* px = reinterpret_cast<float4*>(P.image) + pix;
-    const bool direct = P.samples == nullptr;
-    float4 prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (valid && direct) prev = *px;
-    const rt_camera_ubo& C = P.cam;
-    float fx = (float)x, fy = (float)y;
-    v3 base = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
-    Path S;
-    Trace T;
-    int f = f0;
-    // 0: start the next frame, 1: tracing, 2: trace done (shade pending), 3: all frames done
-    int state = (valid && f < f1) ? 0 : 3;
-    for (;;) {
-        // ---- start paths (a path can end at once when max_depth <= 0)
-        while (state == 0) {
-            unsigned long long t0 = STATS ? clock64() : 0;
-            if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
-            start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, base);
-            if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
-            if (begin_trace(P, S, T)) {
-                state = 1;
-            } else {
-                v3 cur = mk3s(0.0f);
-                if (direct) {
-                    int fc = P.first_frame + f;
-                    float n1 = (float)(fc - 1), n = (float)fc;
-                    prev.x = (prev.x * n1 + cur.x) / n;
-                    prev.y = (prev.y * n1 + cur.y) / n;
-                    prev.z = (prev.z * n1 + cur.z) / n;
-                    prev.w = 1.0f;
-                } else {
-                    P.samples[(size_t)f * P.n_pixels + pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                }
-                f++;
-                state = (f < f1) ? 0 : 3;
-            }
+// Ordered chunks (a launch over few tiles per resident wave, e.g. the stripe set
+// of one of N GPUs): the work unit is one 8x8 tile x one chunk of the launch's
+// frames, unit = chunk * n_tiles + tile, so chunk k of a tile is dequeued after
+// chunk k-1.  The wave that takes chunk k > 0 waits until chunk k-1 of its tile
+// is published, then continues that tile's running mean from the image: the
+// reference's per-frame formula in frame order, so the same bits as one chunk.
+// Publication follows the agent-scope release/acquire recipe of
+// cdna_hip_programming.md §6 G16: the producing wave's plain image stores,
+// vmcnt(0), release fence, vmcnt(0), then one relaxed agent-scope store of the
+// tile's chunk count; the consumer polls that word relaxed (with s_sleep), then
+// one acquire fence, then plain loads.  The unit it waits for was dequeued
+// earlier by a running wave that waits only on earlier units, so the chain ends
+// at chunk 0; the poll is still bounded (RT_CHUNK_WAIT_TICKS of the 100 MHz
+// real-time clock) and a timeout sets P.fault, which rt_sync reports.
+#define RT_CHUNK_WAIT_TICKS 3000000000ull   // 30 s
+typedef __attribute__((address_space(1))) unsigned gu32;   // global (never flat) accesses to shared words
+// tile and chunk are wave-uniform (readfirstlane): every lane polls / stores the
+// same word with the same value, so there is no lane-divergent control flow here
+__device__ __forceinline__ void wait_chunk(const KP& P, int tile, int chunk) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    gu32* w = (gu32*)(P.tile_done + tile);
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
+           (unsigned)chunk) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > RT_CHUNK_WAIT_TICKS) {
+            __hip_atomic_store((gu32*)P.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
         }
-        // ---- traversal stages until enough lanes wait for shading
-        for (;;) {
-            const bool wave_exact = __ballot(state == 1 && T.exact) != 0;   // uniform
-            unsigned long long t0 = STATS ? clock64() : 0;
-            for (;;) {
-                bool walking = state == 1 && T.ni != RT_NODE_END;
-                bool need = walking && T.qn == 0;
-                if (__ballot(need) == 0) break;
-                bool want = walking && (T.qn == 0 || (T.spec && T.qn < Q));
-                if (STATS) st_pred(st, want, ST_NODE_IT, ST_NODE_LN);
-                if (want) node_step(nodes, T, S.o, wave_exact);
-            }
-            if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
-            bool pend = state == 1 && T.qn > 0;
-            if (__ballot(pend) != 0) {
-                unsigned long long t1 = STATS ? clock64() : 0;
-                if (STATS) st_pred(st, pend, ST_LEAF_IT, ST_LEAF_LN);
-                if (pend) leaf_stage<STATS>(P, nodes, S, T, fx, fy, st);
-                if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-            }
-            if (state == 1 && T.ni == RT_NODE_END && T.qn == 0) state = 2;
-            unsigned long long m_wait = __ballot(state == 2);
-            if (__popcll(m_wait) >= P.shade_k || __ballot(state == 1) == 0) break;
-        }
-        // ---- shading (the rest of ray_color's loop body, compute.glsl:307-340)
-        if (state == 2) {
-            unsigned long long ts = STATS ? clock64() : 0;
-            if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
-            const Hit& h = T.h;
-            if (h.uv_kind_idx != 0) {
-                bool sph = (h.uv_kind_idx >> 16) == 1;
-                v3 up = add3(S.o, scale3(S.d, h.uv_a));
-                S.uvs.kind_idx = h.uv_kind_idx;
-                S.uvs.a = sph ? up.x : h.uv_a;
-                S.uvs.b = sph ? up.y : h.uv_b;
-                S.uvs.c = sph ? up.z : S.uvs.c;
-            }
-            v3 cur;
-            bool done;
-            if (!T.has) {
-                cur = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
-                done = true;
-            } else {
-                done = shade(P, S, h, fx, fy, cur);
-            }
-            if (!done) {
-                if (begin_trace(P, S, T)) state = 1;
-                else { cur = mk3s(0.0f); done = true; }
-            }
-            if (done) {
-                if (direct) {
-                    int fc = P.first_frame + f;
-                    float n1 = (float)(fc - 1), n = (float)fc;
-                    prev.x = (prev.x * n1 + cur.x) / n;
-                    prev.y = (prev.y * n1 + cur.y) / n;
-                    prev.z = (prev.z * n1 + cur.z) / n;
-                    prev.w = 1.0f;
-                } else {
-                    P.samples[(size_t)f * P.n_pixels + pix] = make_float4(cur.x, cur.y, cur.z, 0.0f);
-                }
-                f++;
-                state = (f < f1) ? 0 : 3;
-            }
-            if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
-        }
-        if (__ballot(state != 3) == 0) break;
     }
-    if (valid && direct) *px = prev;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void publish_chunk(const KP& P, int tile, int chunk) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store((gu32*)(P.tile_done + tile), (unsigned)(chunk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Persistent kernel: one resident grid; each workgroup stages the threaded BVH
-// (32 B/node, 57 KB for scene 8) in LDS once, then each wave repeatedly takes
-// the next work unit from a device-wide counter (one returning atomic per
-// unit) until the counter passes the last unit — a condition every wave
-// reaches.  A unit is one 8x8 pixel tile x one chunk of the launch's frames
-// (unit = chunk * n_tiles + tile), so a launch over few tiles (a narrow stripe
-// set at N GPUs) still has many more units than resident waves.
-template <int WW, int MINW, bool STATS, bool LDSN, int BLOCK, int DECQ = 0, int SMODE = 0, int FAST = 0,
-          bool LP = false>
+// Persistent kernel: one resident grid; each workgroup stages the BVH (link
+// format, 57 KB for scene 8), the Perlin table and the media records in LDS
+// once, then each wave repeatedly takes the next work unit from a device-wide
+// counter (one returning atomic per unit) until the counter passes the last
+// unit — a condition every wave reaches.
+//   LINK: link-format node loop (variant 0/37) vs threaded meta nodes (30);
+//   LDSN: the nodes are staged in LDS (else read from global memory);
+//   FAST: the exact near-first stack walk (variant 61) with the reference walk
+//         as its fallback.
+template <bool LINK, int MINW, bool STATS, bool LDSN, int BLOCK, bool FAST>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
+    __shared__ float4 s_acc[BLOCK];   // per lane: the pixel's running mean during a unit (RT_LDS_ACC_BYTES)
     __shared__ unsigned long long s_stats[STATS ? BLOCK / 64 : 1][STATS ? ST_N : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1632,15 +1356,15 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         for (int k = tid; k < (BLOCK / 64) * ST_N; k += BLOCK) (&s_stats[0][0])[k] = 0;
         st = s_stats[tid / 64];
     }
-    // FAST 2 keeps its two-child tree + stack in LDS (the reference nodes stay in
+    // FAST keeps its two-child tree + stack in LDS (the reference nodes stay in
     // global memory: leaf checks and the rare exact walk); otherwise LDSN stages
-    // the reference's threaded nodes
+    // the reference's nodes, then the Perlin table and the media records
     FastCtx fc;
     fc.inner = P.f2inner;
     fc.leaves = P.f2leaves;
     fc.stack = nullptr;
     fc.stride = BLOCK;
-    if (FAST == 2) {
+    if (FAST) {
         const int n4 = 4 * P.n_f2inner, nl4 = (P.n_f2leaves + 1) / 2;
         if (LDSN) {
             for (int k = tid; k < n4; k += BLOCK) s_nodes[k] = P.f2inner[k];
@@ -1657,8 +1381,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             fc.stack = reinterpret_cast<short*>(s_nodes) + tid;
         }
     } else if (LDSN) {
-        const float4* g = (WW & 8) ? P.lnodes : reinterpret_cast<const float4*>(P.nodes);
-        const int nf4 = (WW & 8) ? P.n_lnode_f4 : 2 * P.n_nodes;
+        const float4* g = LINK ? P.lnodes : reinterpret_cast<const float4*>(P.nodes);
+        const int nf4 = LINK ? P.n_lnode_f4 : 2 * P.n_nodes;
         for (int k = tid; k < nf4; k += BLOCK) s_nodes[k] = g[k];
         if (P.perlin_lds >= 0) {   // the Perlin table after the nodes (host-sized launch)
             const rt_dtex& T = P.tex[P.perlin_slot];
@@ -1666,12 +1390,6 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             float* dst = reinterpret_cast<float*>(s_nodes + P.perlin_lds);
             for (int k = tid; k < T.w * T.h; k += BLOCK) dst[k] = src[k];
         }
-        if (P.sph_lds >= 0)   // spheres: center1 + texture, center_vec + radius
-            for (int k = tid; k < 2 * P.n_spheres; k += BLOCK)
-                s_nodes[P.sph_lds + k] = reinterpret_cast<const float4*>(P.spheres + k / 2)[k % 2];
-        if (P.boxc_lds >= 0)   // the boxes' canonical plane tails
-            for (int k = tid; k < 3 * P.n_boxes; k += BLOCK)
-                s_nodes[P.boxc_lds + k] = P.dboxes[(size_t)(k / 3) * RT_DBOX_F4 + 18 + k % 3];
         if (P.media_lds >= 0) {   // per medium: (boundary idx, type, -1/density, phase), sphere A, B
             for (int k = tid; k < 3 * P.n_media; k += BLOCK) {
                 const rt_medium& m = P.media[k / 3];
@@ -1687,29 +1405,29 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
     }
     if (LDSN || STATS) __syncthreads();
     if (STATS) t_begin = clock64();
-    const float4* __restrict__ rnodes = (LDSN && FAST != 2) ? s_nodes : reinterpret_cast<const float4*>(P.nodes);
+    const float4* __restrict__ rnodes = (LDSN && !FAST) ? s_nodes : reinterpret_cast<const float4*>(P.nodes);
     const int tiles_x = (P.width + 7) >> 3;
     const int n_tiles = tiles_x * ((P.local_rows + 7) >> 3);
     const int n_units = n_tiles * P.n_chunks;
     for (;;) {
         int unit = 0;
         if (lane == 0) unit = atomicAdd(P.tile_counter, 1);
-        unit = __shfl(unit, 0);
+        unit = __builtin_amdgcn_readfirstlane(__shfl(unit, 0));   // wave-uniform (scalar)
         if (unit >= n_units) break;
         const int chunk = unit / n_tiles, tile = unit - chunk * n_tiles;
         const int f0 = chunk * P.chunk_frames;
         const int f1 = min(P.n_frames, f0 + P.chunk_frames);
-        int x = (tile % tiles_x) * 8 + (lane & 7);
-        int lr = (tile / tiles_x) * 8 + (lane >> 3);
-        if (DECQ > 0) {
-            // every lane enters (the stages are wave-wide); invalid lanes idle
-            bool valid = x < P.width && lr < P.local_rows;
-            int xc = valid ? x : 0, lc = valid ? lr : 0;
-            if (LDSN) render_pixel_dec<DECQ, STATS>(P, s_nodes, xc, lc, f0, f1, valid, st);
-            else render_pixel_dec<DECQ, STATS>(P, reinterpret_cast<const float4*>(P.nodes), xc, lc, f0, f1, valid, st);
-        } else if (x < P.width && lr < P.local_rows) {
-            render_pixel<WW, STATS, SMODE, FAST, LP>(P, rnodes, fc, x, lr, f0, f1, st);
+        const int x = (tile % tiles_x) * 8 + (lane & 7);
+        const int lr = (tile / tiles_x) * 8 + (lane >> 3);
+        const bool valid = x < P.width && lr < P.local_rows;   // lane 0 (the tile's corner) always is
+        if (chunk > 0) wait_chunk(P, tile, chunk);
+        if (valid) {
+            float4* px = reinterpret_cast<float4*>(P.image) + (size_t)lr * P.width + x;
+            s_acc[tid] = *px;
+            render_pixel<LINK, STATS, FAST>(P, rnodes, fc, x, lr, f0, f1, s_acc + tid, st);
+            *px = s_acc[tid];
         }
+        if (chunk + 1 < P.n_chunks) publish_chunk(P, tile, chunk);
     }
     if (STATS) {
         st_add(st, ST_TOTAL, clock64() - t_begin);
@@ -1720,282 +1438,6 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             atomicAdd(P.stats + tid, v);
         }
     }
-}
-
-// Chunked mode epilogue: the running mean of compute.glsl:355 over the
-// launch's frames, in frame order, per pixel: (prev*(n-1)+cur)/n.
-__global__ void __launch_bounds__(256) fold_kernel(const KP* __restrict__ Pp) {
-    const KP& P = *Pp;
-    const size_t pix = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (pix >= P.n_pixels) return;
-    float4* px = reinterpret_cast<float4*>(P.image) + pix;
-    float4 prev = *px;
-    const float4* s = P.samples + pix;
-    for (int f = 0; f < P.n_frames; f++) {
-        float4 cur = s[(size_t)f * P.n_pixels];
-        int fc = P.first_frame + f;
-        float n1 = (float)(fc - 1), n = (float)fc;
-        prev.x = (prev.x * n1 + cur.x) / n;
-        prev.y = (prev.y * n1 + cur.y) / n;
-        prev.z = (prev.z * n1 + cur.z) / n;
-        prev.w = 1.0f;
-    }
-    *px = prev;
-}
-
-// ===========================================================================
-// Wavefront pipeline (variant 50).  The launch's (pixel, frame) paths flow
-// through two queues of in-flight paths (rt_device.h: WF_REC_F4 float4 per
-// record) and two kernels per bounce:
-//   wf_trace  — persistent; each lane walks one queued ray and, when its walk
-//               ends, writes the hit record and fetches the next queued ray
-//               (dynamic ray fetch), so lanes do not idle behind the wave's
-//               longest walk; lanes with finite 1/dir keep walking past a hit
-//               leaf (queue of WF_Q leaves, exact re-test on dequeue — the
-//               argument is at struct Trace above);
-//   wf_shade  — one thread per queued path: the rest of ray_color's loop body
-//               (compute.glsl:307-340); a continuing path is appended to the
-//               other queue, a finished one writes its colour to
-//               samples[frame][pixel] and claims the next unstarted path.
-// Per path, the same operations in the same order as the megakernel, so the
-// same bits; fold_kernel then applies the running mean in frame order.
-// Path ids enumerate frame-major, 8x8-tile order within a frame.
-
-__device__ __forceinline__ unsigned long long lanemask_lt() {
-    const unsigned lane = __lane_id();
-    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
-}
-
-// path id -> (local pixel index, frame); false for a padding pixel of a ragged tile
-__device__ __forceinline__ bool wf_decode(const KP& P, unsigned long long pid, int& x, int& lr, int& f) {
-    const int tiles_x = (P.width + 7) >> 3;
-    const unsigned long long per_frame = (unsigned long long)P.wf_tiles * 64ull;
-    f = (int)(pid / per_frame);
-    unsigned long long r = pid - (unsigned long long)f * per_frame;
-    int tile = (int)(r >> 6), within = (int)(r & 63);
-    x = (tile % tiles_x) * 8 + (within & 7);
-    lr = (tile / tiles_x) * 8 + (within >> 3);
-    return x < P.width && lr < P.local_rows;
-}
-
-__device__ __forceinline__ void wf_pixel_xy(const KP& P, int x, int lr, float& fx, float& fy) {
-    int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
-    int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
-    fx = (float)x;
-    fy = (float)y;
-}
-
-// queue record: a = (o, time), b = (d, rf), c = (acc, uvs.a), e = (uvs.b, uvs.c, uvs.kind_idx, depth),
-//               g = (x, lr, frame, 0)
-__device__ __forceinline__ void wf_store(float4* __restrict__ rec, const Path& S, int x, int lr, int f) {
-    rec[0] = make_float4(S.o.x, S.o.y, S.o.z, S.time);
-    rec[1] = make_float4(S.d.x, S.d.y, S.d.z, S.rf);
-    rec[2] = make_float4(S.acc.x, S.acc.y, S.acc.z, S.uvs.a);
-    rec[3] = make_float4(S.uvs.b, S.uvs.c, __int_as_float(S.uvs.kind_idx), __int_as_float(S.depth));
-    rec[4] = make_float4(__int_as_float(x), __int_as_float(lr), __int_as_float(f), 0.0f);
-}
-
-template <int Q, int MINW, int BLOCK, bool LDSN>
-__global__ void __launch_bounds__(BLOCK, MINW) wf_trace(const KP* __restrict__ Pp, int in) {
-    const KP& P = *Pp;
-    extern __shared__ float4 s_nodes[];
-    unsigned* ctr = P.wf_ctr;
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[1 - in] = 0u;   // the shade after us appends there
-    if (LDSN) {
-        const float4* g = reinterpret_cast<const float4*>(P.nodes);
-        for (int k = threadIdx.x; k < 2 * P.n_nodes; k += BLOCK) s_nodes[k] = g[k];
-        __syncthreads();
-    }
-    const float4* __restrict__ nodes = LDSN ? s_nodes : reinterpret_cast<const float4*>(P.nodes);
-    const int n = (int)ctr[in];
-    const float4* __restrict__ q = P.wf_q[in];
-    float4* __restrict__ hits = P.wf_hits;
-    const unsigned lane = __lane_id();
-    int e = -1;            // queue entry this lane walks
-    bool drained = false;  // wave-uniform: the queue has no entries left
-    v3 o = mk3s(0.0f), d = mk3s(0.0f);
-    float time = 0.0f, rf = 0.0f, fx = 0.0f, fy = 0.0f;
-    Trace T;
-    T.ni = RT_NODE_END; T.qn = 0; T.q = 0; T.has = false; T.exact = false; T.spec = false; T.tmax = 0.0f;
-    T.a = 0.0f; T.inv = mk3s(0.0f);
-    T.h.t = 0.0f; T.h.type = 0; T.h.idx = 0; T.h.face = 0; T.h.uv_kind_idx = 0; T.h.uv_a = 0.0f; T.h.uv_b = 0.0f;
-    for (;;) {
-        // ---- refill idle lanes from the queue (one atomic per wave)
-        unsigned long long idle = __ballot(e < 0);
-        if (!drained && __popcll(idle) >= P.wf_refill) {
-            int base = 0;
-            const int first = __ffsll((long long)idle) - 1;
-            if ((int)lane == first) base = (int)atomicAdd(&ctr[2], (unsigned)__popcll(idle));
-            base = __shfl(base, first);
-            if (base + __popcll(idle) >= n) drained = true;
-            if (e < 0) {
-                int k = base + __popcll(idle & lanemask_lt());
-                if (k < n) {
-                    e = k;
-                    const float4* r = q + (size_t)k * WF_REC_F4;
-                    float4 ra = r[0], rb = r[1], rg = r[4];
-                    o = f3(ra); time = ra.w;
-                    d = f3(rb); rf = rb.w;
-                    wf_pixel_xy(P, __float_as_int(rg.x), __float_as_int(rg.y), fx, fy);
-                    // trace_through_bvh's prologue (compute.glsl:226-236)
-                    T.h.t = 0.0f; T.h.type = 0; T.h.idx = 0; T.h.face = 0;
-                    T.h.uv_kind_idx = 0; T.h.uv_a = 0.0f; T.h.uv_b = 0.0f;
-                    T.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-                    T.a = g_dot(d, d);
-                    T.tmax = RT_INFINITY;
-                    T.has = false;
-                    T.q = 0;
-                    T.qn = 0;
-                    bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);   // Q1 corner: no hit, no rand()
-                    T.ni = (dir_zero || P.n_nodes == 0) ? RT_NODE_END : 0u;
-                    T.exact = (T.inv.x == -INFINITY) || (T.inv.y == -INFINITY) || (T.inv.z == -INFINITY);
-                    T.spec = P.spec_ok && fabsf(T.inv.x) < INFINITY && fabsf(T.inv.y) < INFINITY &&
-                             fabsf(T.inv.z) < INFINITY;
-                }
-            }
-        }
-        if (__ballot(e >= 0) == 0) {
-            if (drained) break;
-            continue;   // every lane idle but entries remain: refill next round
-        }
-        // ---- node steps until every walking lane has a leaf queued (or walked out)
-        const bool wave_exact = __ballot(e >= 0 && T.exact) != 0;
-        for (;;) {
-            bool walking = e >= 0 && T.ni != RT_NODE_END;
-            if (__ballot(walking && T.qn == 0) == 0) break;
-            if (walking && (T.qn == 0 || (T.spec && T.qn < Q))) node_step(nodes, T, o, wave_exact);
-        }
-        // ---- one queued leaf per lane, exact re-test, prims in order
-        if (e >= 0 && T.qn > 0) {
-            const uint32_t i = (uint32_t)(T.q & 0xFFFFu);
-            T.q >>= 16;
-            T.qn--;
-            float4 n0 = nodes[2 * i], n1 = nodes[2 * i + 1];
-            bool hitn;
-            if (!T.exact) {
-                hitn = aabb_fast(n0, n1, o, T.inv, 0.001f, T.tmax);
-            } else {
-                float lo = 0.001f, hi = T.tmax;
-                slab(n0.x, n0.y, o.x, T.inv.x, lo, hi);
-                slab(n0.z, n0.w, o.y, T.inv.y, lo, hi);
-                slab(n1.x, n1.y, o.z, T.inv.z, lo, hi);
-                hitn = !(hi <= lo);
-            }
-            if (hitn)
-                leaf_prims<false>(P, __float_as_uint(n1.z), __float_as_uint(n1.w), o, d, T.a, time, 0.001f, T.tmax,
-                                  rf, fx, fy, T.h, T.has, nullptr);
-        }
-        // ---- finished walks: write the hit record, free the lane
-        if (e >= 0 && T.ni == RT_NODE_END && T.qn == 0) {
-            float4* hr = hits + (size_t)e * WF_HIT_F4;
-            hr[0] = make_float4(T.h.t, T.h.uv_a, T.h.uv_b, rf);
-            hr[1] = make_float4(__int_as_float(T.has ? 1 : 0), __int_as_float(T.h.type | (T.h.face << 8)),
-                                __int_as_float(T.h.idx), __int_as_float(T.h.uv_kind_idx));
-            e = -1;
-        }
-    }
-}
-
-// Lanes with `need` start the next unstarted paths (one atomic per wave and
-// round); on return a lane has `push` set when it holds a started path (S and
-// x, lr, f set) that needs a walk.  Called by every active lane of the wave.
-__device__ __forceinline__ bool wf_claim(const KP& P, bool need, Path& S, int& x, int& lr, int& f) {
-    bool push = false;
-    for (;;) {
-        unsigned long long m = __ballot(need);
-        if (m == 0) return push;
-        const int first = __ffsll((long long)m) - 1;
-        unsigned long long base = 0;
-        if ((int)__lane_id() == first) base = atomicAdd(P.wf_next, (unsigned long long)__popcll(m));
-        base = __shfl(base, first);
-        if (need) {
-            unsigned long long pid = base + (unsigned long long)__popcll(m & lanemask_lt());
-            if (pid >= P.wf_total) {
-                need = false;
-            } else if (wf_decode(P, pid, x, lr, f)) {
-                float fx, fy;
-                wf_pixel_xy(P, x, lr, fx, fy);
-                const rt_camera_ubo& C = P.cam;
-                v3 cb = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
-                start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, cb);
-                if (S.depth >= P.max_depth) {   // compute.glsl:304 loop bound: final_color stays 0
-                    P.samples[(size_t)f * P.n_pixels + (size_t)lr * P.width + x] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                } else {
-                    S.depth++;
-                    push = true;
-                    need = false;
-                }
-            }
-        }
-    }
-}
-
-__global__ void __launch_bounds__(256) wf_shade(const KP* __restrict__ Pp, int in, int gen) {
-    const KP& P = *Pp;
-    unsigned* ctr = P.wf_ctr;
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[2] = 0u;   // the next wf_trace's fetch head
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int n = gen ? 0 : (int)ctr[in];
-    if (i >= P.wf_slots || (!gen && i >= n)) return;   // whole waves exit together past the end
-    Path S;
-    int x = 0, lr = 0, f = 0;
-    bool push;
-    if (i < n) {
-        const float4* r = P.wf_q[in] + (size_t)i * WF_REC_F4;
-        const float4* hr = P.wf_hits + (size_t)i * WF_HIT_F4;
-        float4 ra = r[0], rb = r[1], rc = r[2], re = r[3], rg = r[4];
-        float4 ha = hr[0], hb = hr[1];
-        S.o = f3(ra); S.time = ra.w;
-        S.d = f3(rb);
-        S.rf = ha.w;   // rand_factor after the walk's medium draws
-        S.acc = f3(rc);
-        S.uvs.a = rc.w; S.uvs.b = re.x; S.uvs.c = re.y; S.uvs.kind_idx = __float_as_int(re.z);
-        S.depth = __float_as_int(re.w);
-        x = __float_as_int(rg.x); lr = __float_as_int(rg.y); f = __float_as_int(rg.z);
-        Hit h;
-        h.t = ha.x; h.uv_a = ha.y; h.uv_b = ha.z;
-        const bool has = __float_as_int(hb.x) != 0;
-        const int tf = __float_as_int(hb.y);
-        h.type = tf & 0xFF; h.face = tf >> 8;
-        h.idx = __float_as_int(hb.z);
-        h.uv_kind_idx = __float_as_int(hb.w);
-        float fx, fy;
-        wf_pixel_xy(P, x, lr, fx, fy);
-        // hit_record.uv as left by this walk (compute.glsl:62)
-        if (h.uv_kind_idx != 0) {
-            bool sph = (h.uv_kind_idx >> 16) == 1;
-            v3 up = add3(S.o, scale3(S.d, h.uv_a));
-            S.uvs.kind_idx = h.uv_kind_idx;
-            S.uvs.a = sph ? up.x : h.uv_a;
-            S.uvs.b = sph ? up.y : h.uv_b;
-            S.uvs.c = sph ? up.z : S.uvs.c;
-        }
-        v3 cur;
-        bool done;
-        if (!has) {
-            cur = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
-            done = true;
-        } else {
-            done = shade(P, S, h, fx, fy, cur);
-        }
-        if (!done) {
-            if (S.depth >= P.max_depth) { cur = mk3s(0.0f); done = true; }
-            else S.depth++;
-        }
-        if (done) P.samples[(size_t)f * P.n_pixels + (size_t)lr * P.width + x] = make_float4(cur.x, cur.y, cur.z, 0.0f);
-        push = !done;
-        if (__ballot(done) != 0) push = wf_claim(P, done, S, x, lr, f) || push;
-    } else {
-        push = wf_claim(P, true, S, x, lr, f);   // initial fill
-    }
-    // append to the other queue: one atomic per wave, contiguous records
-    unsigned long long m = __ballot(push);
-    if (m == 0) return;
-    const int first = __ffsll((long long)m) - 1;
-    int base = 0;
-    if ((int)__lane_id() == first) base = (int)atomicAdd(&ctr[1 - in], (unsigned)__popcll(m));
-    base = __shfl(base, first);
-    if (push) wf_store(P.wf_q[1 - in] + (size_t)(base + __popcll(m & lanemask_lt())) * WF_REC_F4, S, x, lr, f);
 }
 
 __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const float* __restrict__ y,
@@ -2040,50 +1482,7 @@ int rt_resident_waves(void) {
     return cus * 2 * (512 / 64);   // default shape: 2 workgroups of 512 per CU
 }
 
-// The wavefront pipeline's host loop: fill, then batches of (trace, shade)
-// until the path queue is empty (one small readback per batch), then the fold.
-template <typename K>
-int wf_grid(K kernel, int block, size_t lds) {
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
-        per_cu = 1;
-    return cus * per_cu;
-}
-
-int launch_wavefront(const rt_kernel_args& a, const rt_kernel_args* d, hipStream_t st, unsigned* host_ctr) {
-    constexpr int WB = 512, WM = 4, WQ = 2;
-    size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
-    const bool fits = lds <= RT_LDS_NODE_BYTES;
-    auto trace_k = fits ? wf_trace<WQ, WM, WB, true> : wf_trace<WQ, WM, WB, false>;
-    if (!fits) lds = 0;
-    const int grid = wf_grid(trace_k, WB, lds);
-    if (grid < 0) return -1;
-    const unsigned shade_blocks = (unsigned)((a.wf_slots + 255) / 256);
-    if (hipMemsetAsync(a.wf_ctr, 0, 4 * sizeof(unsigned), st) != hipSuccess) return -1;
-    if (hipMemsetAsync(a.wf_next, 0, sizeof(unsigned long long), st) != hipSuccess) return -1;
-    hipLaunchKernelGGL(wf_shade, dim3(shade_blocks), dim3(256), 0, st, d, 1, 1);   // fill queue 0
-    int in = 0;
-    for (int batch = 0;; batch++) {
-        const int B = batch == 0 ? 8 : 4;
-        for (int k = 0; k < B; k++) {
-            hipLaunchKernelGGL(trace_k, dim3(grid), dim3(WB), lds, st, d, in);
-            hipLaunchKernelGGL(wf_shade, dim3(shade_blocks), dim3(256), 0, st, d, in, 0);
-            in ^= 1;
-        }
-        if (hipMemcpyAsync(host_ctr, a.wf_ctr, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st) != hipSuccess)
-            return -1;
-        if (hipStreamSynchronize(st) != hipSuccess) return -1;
-        if (host_ctr[in] == 0) break;
-        if (batch > 20000) return -1;   // a path ends within max_depth bounces: never reached
-    }
-    unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);
-    hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), 0, st, d);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream, unsigned* host_ctr) {
+int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.
@@ -2092,118 +1491,48 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     hipStream_t st = (hipStream_t)stream;
     if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
     const rt_kernel_args* d = (const rt_kernel_args*)dargs;
-    // Variants (A/B only; all bit-identical):
-    //   0: variant 37 (30 when the link format is unavailable or does not fit LDS)
-    //   37: 30 over the link-format nodes (explicit hit / miss successors, packed slab); 38 stats of 37
-    //   30: while-while, fast slab, branch-free node step, 512 threads / 4 waves per SIMD
-    //   35 = 30 specialised for direct or chunked launches (SMODE)
-    //   31 stats of 30;  10 while-while (exact slab) 512/4w;  19 stats of 10
-    //   12 = 30 with global-memory nodes;  15 = 30 at 768 threads / 3 waves
-    if (a.variant == 50) {
-        if (!a.samples || !a.wf_q[0] || !host_ctr) return -1;
-        return launch_wavefront(a, d, st, host_ctr);
-    }
+    // the work-unit counter, then (ordered chunks) the tiles' published chunk counts
+    const int n_tiles = ((a.width + 7) / 8) * ((a.local_rows + 7) / 8);
     if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
-    size_t lds = (size_t)a.n_nodes * sizeof(rt_dnode);
-    bool fits = lds <= RT_LDS_NODE_BYTES;
-    // default shapes (0, 30): + the Perlin table the host placed after the nodes
-    const size_t lds_p = a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
-                         : lds + (a.perlin_lds >= 0 ? (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h * 4 : 0);
-    // variant 37: link-format nodes, then the Perlin table and media as placed by the host
-    const size_t lds_l = a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
-                         : a.perlin_lds >= 0 ? ((size_t)a.perlin_lds + (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h / 4) * 16
-                                             : (size_t)a.n_lnode_f4 * 16;
+    if (a.n_chunks > 1 && hipMemsetAsync(a.tile_done, 0, sizeof(unsigned) * (size_t)n_tiles, st) != hipSuccess)
+        return -1;
+    // Variants (RT_KERNEL_VARIANT; all bit-identical, tests/test_gpu_boundary.py):
+    //   0 = 37: link-format nodes in LDS (+ the Perlin table and media records), 512 threads,
+    //           4 waves per SIMD; 38 its stats twin.  Falls back to 30 when the link format is
+    //           unavailable (> 2047 nodes) or does not fit LDS.
+    //   30: threaded nodes with the meta word (in LDS when they fit, else global); 31 stats twin.
+    //   61: the exact near-first stack walk (tree and stacks in LDS); 69 stats twin.
+    const size_t lds_t = (size_t)a.n_nodes * sizeof(rt_dnode);   // threaded nodes
+    const bool fits_t = lds_t <= RT_LDS_NODE_BYTES;
+    // after the nodes, as placed by the host: the Perlin table, then the media records
+    const size_t extra_end = a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
+                             : a.perlin_lds >= 0
+                                 ? ((size_t)a.perlin_lds + (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h / 4) * 16
+                                 : 0;
+    const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
+    const size_t lds_p = lds_t > extra_end ? lds_t : extra_end;
+    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69;
     int rc;
-    switch (a.variant) {
-        case 10: rc = fits ? launch_persistent(render_persistent<1, 4, false, true, 512>, 512, lds, d, st)
-                           : launch_persistent(render_persistent<1, 4, false, false, 512>, 512, 0, d, st); break;
-        case 19: rc = fits ? launch_persistent(render_persistent<1, 4, true, true, 512>, 512, lds, d, st)
-                           : launch_persistent(render_persistent<1, 4, true, false, 512>, 512, 0, d, st); break;
-        case 12: rc = launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
-        case 15: rc = fits ? launch_persistent(render_persistent<3, 3, false, true, 768>, 768, lds, d, st)
-                           : launch_persistent(render_persistent<3, 3, false, false, 768>, 768, 0, d, st); break;
-        case 41: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 1>, 512, lds, d, st)
-                           : launch_persistent(render_persistent<3, 4, false, false, 512, 1>, 512, 0, d, st); break;
-        case 42: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 2>, 512, lds, d, st)
-                           : launch_persistent(render_persistent<3, 4, false, false, 512, 2>, 512, 0, d, st); break;
-        case 43: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 3>, 512, lds, d, st)
-                           : launch_persistent(render_persistent<3, 4, false, false, 512, 3>, 512, 0, d, st); break;
-        case 49: rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512, 2>, 512, lds, d, st)
-                           : launch_persistent(render_persistent<3, 4, true, false, 512, 2>, 512, 0, d, st); break;
-        case 31: rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512>, 512, lds, d, st)
-                           : launch_persistent(render_persistent<3, 4, true, false, 512>, 512, 0, d, st); break;
-        case 32: rc = fits ? launch_persistent(render_persistent<7, 4, false, true, 512, 0, 0>, 512, lds, d, st)
-                           : launch_persistent(render_persistent<7, 4, false, false, 512, 0, 0>, 512, 0, d, st); break;
-        case 33: rc = fits ? launch_persistent(render_persistent<3, 5, false, true, 640, 0, 0>, 640, lds, d, st)
-                           : launch_persistent(render_persistent<3, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
-        case 34: rc = fits ? launch_persistent(render_persistent<7, 5, false, true, 640, 0, 0>, 640, lds, d, st)
-                           : launch_persistent(render_persistent<7, 5, false, false, 640, 0, 0>, 640, 0, d, st); break;
-        case 36: {   // one 1024-thread workgroup per CU: nodes, Perlin, media, spheres, box planes in LDS
-            size_t l36 = (size_t)2 * a.n_nodes;
-            if (a.perlin_lds >= 0) l36 = (size_t)a.perlin_lds + ((size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h + 3) / 4;
-            if (a.media_lds >= 0) l36 = (size_t)a.media_lds + 3 * (size_t)a.n_media;
-            if (a.sph_lds >= 0) l36 = (size_t)a.sph_lds + 2 * (size_t)a.n_spheres;
-            if (a.boxc_lds >= 0) l36 = (size_t)a.boxc_lds + 3 * (size_t)a.n_boxes;
-            rc = (l36 * 16 <= RT_LDS_CU_BYTES && a.sph_lds >= 0)
-                     ? launch_persistent(render_persistent<3, 4, false, true, 1024, 0, 0, 0, true>, 1024, l36 * 16, d, st)
-                     : launch_persistent(render_persistent<3, 4, false, false, 1024>, 1024, 0, d, st);
-            break;
-        }
-        default:   // 0 = 37
-        case 37:   // 30 over the link-format nodes in LDS (up to 80 KB with the Perlin table and media)
-        case 38:   // stats twin
-            if (a.n_lnode_f4 > 0 && lds_l <= RT_LDS_FAST_BYTES) {
-                rc = a.variant == 38 ? launch_persistent(render_persistent<11, 4, true, true, 512>, 512, lds_l, d, st)
-                                     : launch_persistent(render_persistent<11, 4, false, true, 512>, 512, lds_l, d, st);
-                break;
-            }
-            rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds_p, d, st)
-                      : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st);
-            break;
-        case 30: rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512>, 512, lds_p, d, st)
-                           : launch_persistent(render_persistent<3, 4, false, false, 512>, 512, 0, d, st); break;
-        case 60:   // exact near-first walk (trace_fast), otherwise as 0
-        case 68:   // stats twin of 60
-            if (a.variant == 68)
-                rc = fits ? launch_persistent(render_persistent<3, 4, true, true, 512, 0, 0, 1>, 512, lds, d, st)
-                          : launch_persistent(render_persistent<3, 4, true, false, 512, 0, 0, 1>, 512, 0, d, st);
-            else if (a.samples)
-                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2, 1>, 512, lds, d, st)
-                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2, 1>, 512, 0, d, st);
-            else
-                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1, 1>, 512, lds, d, st)
-                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1, 1>, 512, 0, d, st);
-            break;
-        case 61:     // exact near-first stack walk over the two-child tree in LDS, otherwise as 0
-        case 69: {   // stats twin of 61
-            const size_t stack_b = (size_t)RT_FAST_STACK * 512 * sizeof(short);
-            const size_t tree_b = (size_t)a.n_f2inner * 64 + (size_t)((a.n_f2leaves + 1) / 2) * 16;
-            const bool in_lds = tree_b + stack_b <= RT_LDS_FAST_BYTES;
-            const size_t l2 = in_lds ? tree_b + stack_b : stack_b;
-            if (a.variant == 69)
-                rc = launch_persistent(render_persistent<3, 4, true, true, 512, 0, 0, 2>, 512, l2, d, st);
-            else if (a.samples)
-                rc = in_lds ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2, 2>, 512, l2, d, st)
-                            : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2, 2>, 512, l2, d, st);
-            else
-                rc = in_lds ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1, 2>, 512, l2, d, st)
-                            : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1, 2>, 512, l2, d, st);
-            break;
-        }
-        case 35:   // 30 specialised for the launch's work split (SMODE; measured 1 ms slower than 30)
-            if (a.samples)
-                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 2>, 512, lds_p, d, st)
-                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 2>, 512, 0, d, st);
-            else
-                rc = fits ? launch_persistent(render_persistent<3, 4, false, true, 512, 0, 1>, 512, lds_p, d, st)
-                          : launch_persistent(render_persistent<3, 4, false, false, 512, 0, 1>, 512, 0, d, st);
-            break;
+    if (a.variant == 61 || a.variant == 69) {
+        const size_t stack_b = (size_t)RT_FAST_STACK * 512 * sizeof(short);
+        const size_t tree_b = (size_t)a.n_f2inner * 64 + (size_t)((a.n_f2leaves + 1) / 2) * 16;
+        const bool in_lds = tree_b + stack_b <= RT_LDS_DYN_BYTES;
+        const size_t l2 = in_lds ? tree_b + stack_b : stack_b;
+        if (stats) rc = in_lds ? launch_persistent(render_persistent<false, 4, true, true, 512, true>, 512, l2, d, st)
+                               : launch_persistent(render_persistent<false, 4, true, false, 512, true>, 512, l2, d, st);
+        else rc = in_lds ? launch_persistent(render_persistent<false, 4, false, true, 512, true>, 512, l2, d, st)
+                         : launch_persistent(render_persistent<false, 4, false, false, 512, true>, 512, l2, d, st);
+    } else if (a.variant != 30 && a.variant != 31 && a.n_lnode_f4 > 0 && lds_l <= RT_LDS_DYN_BYTES) {
+        rc = stats ? launch_persistent(render_persistent<true, 4, true, true, 512, false>, 512, lds_l, d, st)
+                   : launch_persistent(render_persistent<true, 4, false, true, 512, false>, 512, lds_l, d, st);
+    } else if (fits_t && lds_p <= RT_LDS_DYN_BYTES) {
+        rc = stats ? launch_persistent(render_persistent<false, 4, true, true, 512, false>, 512, lds_p, d, st)
+                   : launch_persistent(render_persistent<false, 4, false, true, 512, false>, 512, lds_p, d, st);
+    } else {
+        rc = stats ? launch_persistent(render_persistent<false, 4, true, false, 512, false>, 512, 0, d, st)
+                   : launch_persistent(render_persistent<false, 4, false, false, 512, false>, 512, 0, d, st);
     }
     if (rc) return rc;
-    if (a.samples) {
-        unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);
-        hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), 0, st, d);
-    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

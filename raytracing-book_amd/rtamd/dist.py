@@ -5,8 +5,8 @@ scene) (random.glsl:2-7, compute.glsl:346), so any row partition renders
 bit-identically to one GPU.  Rank k owns the stripes s with s % world == k
 (SURVEY §8e).  During rendering there is no inter-GPU traffic; at the end each
 rank contributes its stripe-compacted, equally padded [padded_rows, W, 4]
-RGBA32F block to one all_gather (RCCL over xGMI with backend "nccl", gloo on
-CPU) and the blocks are de-interleaved into the full image.
+RGBA32F block to one gather to rank 0 (RCCL over xGMI with backend "nccl",
+gloo on CPU), and rank 0 de-interleaves the blocks into the full image.
 """
 import numpy as np
 import torch
@@ -34,19 +34,24 @@ def init_from_env(backend=None):
 
 
 def gather_image(local_block, height, world, stripe_rows):
-    """All-gather the [padded_rows, W, 4] blocks and de-interleave (rank 0 and others)."""
+    """Gather the ranks' [padded_rows, W, 4] blocks to rank 0 and de-interleave.
+
+    Returns the [H, W, 4] image on rank 0 and None on every other rank: only
+    rank 0 receives the blocks (one gather, not an all-gather) and only rank 0
+    copies them to the host."""
     if world == 1:
         rows = local_rows(height, 0, 1, stripe_rows)
         return local_block[:rows].cpu().numpy()
     padded = padded_local_rows(height, world, stripe_rows)
     assert local_block.shape[0] == padded
-    if dist.get_backend() == "nccl":
-        out = torch.empty((world,) + tuple(local_block.shape), dtype=local_block.dtype, device=local_block.device)
-        dist.all_gather_into_tensor(out, local_block.contiguous())
-        g = out.cpu().numpy()
-    else:
-        blk = local_block.detach().cpu().contiguous()   # gloo gathers host tensors
+    rank = dist.get_rank()
+    blk = local_block.contiguous()
+    if dist.get_backend() != "nccl":
+        blk = blk.detach().cpu()   # gloo gathers host tensors
+    if rank == 0:
         parts = [torch.empty_like(blk) for _ in range(world)]
-        dist.all_gather(parts, blk)
-        g = np.stack([p.cpu().numpy() for p in parts])
-    return deinterleave(g, height, world, stripe_rows)
+        dist.gather(blk, gather_list=parts, dst=0)
+        g = torch.stack(parts).cpu().numpy()
+        return deinterleave(g, height, world, stripe_rows)
+    dist.gather(blk, dst=0)
+    return None

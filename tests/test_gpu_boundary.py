@@ -137,14 +137,14 @@ def test_bound_torch_image_and_stream(gpu):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
-VARIANTS = [0, 10, 12, 15, 30, 32, 35, 36, 37, 41, 42, 43, 50, 60, 61]
+VARIANTS = [0, 30, 61]   # link-format walk (default), threaded meta walk, exact near-first walk
 
 
 @pytest.mark.parametrize("chunk_target", ["0", "1", "16", "100000"])
 def test_all_kernel_variants_identical(gpu, monkeypatch, chunk_target):
-    """Every launch shape of the kernel (RT_KERNEL_VARIANT, used for A/B timing) and
-    every work split (RT_CHUNK_TARGET: 0 = direct running mean in registers, else
-    tile x frame-chunk units with the fold epilogue) renders the same bits."""
+    """Every launch shape of the kernel (RT_KERNEL_VARIANT) and every work split
+    (RT_CHUNK_TARGET: 0 = one unit per tile with all frames, else tile x ordered
+    frame-chunk units handed over between waves) renders the same bits."""
     s = rtamd.Scene(8, 40, 24, seed=1)
     ref = oracle_image(s, 6)
     monkeypatch.setenv("RT_CHUNK_TARGET", chunk_target)
@@ -152,6 +152,16 @@ def test_all_kernel_variants_identical(gpu, monkeypatch, chunk_target):
         monkeypatch.setenv("RT_KERNEL_VARIANT", str(v))
         out = gpu_image(s, 6)
         assert bit_equal(out, ref), f"variant {v}, chunk target {chunk_target}: {mismatch_report(out, ref)}"
+
+
+def test_ordered_chunk_chain_small_image(gpu, monkeypatch):
+    """Few tiles, many chunks: each of the 15 tiles' 200 one-frame chunks waits for the
+    previous one (the hand-off is on the critical path), over 2 launches (256 + 44 frames)."""
+    s = rtamd.Scene(8, 40, 24, seed=1)
+    ref = oracle_image(s, 300, spp=300)
+    monkeypatch.setenv("RT_CHUNK_TARGET", "100000")
+    out = gpu_image(s, 300, spp=300)
+    assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
 def test_stats_build_renders_same_bits(gpu):

@@ -5,8 +5,10 @@ the full image on the GPU and checks it three ways:
   * sampled rows: the oracle renders a few whole 8-row stripes of the same image
     (its stripe partition: world = n_stripes, rank = stripe) and those rows must
     match the GPU image bit for bit;
-  * work-split independence: the direct launch (running mean in registers) and
-    the tile x frame-chunk launch (per-frame colours + fold) give the same bits;
+  * work-split independence: one unit per tile (all frames of the launch in
+    one wave) and tile x ordered frame-chunk units (the running mean handed
+    from wave to wave through the image, rt_kernel.hip wait_chunk) give the
+    same bits;
   * partition independence: N stripe-partitioned contexts (one per rank, as
     one process per GPU would run them) reassemble to the 1-context image.
 """
@@ -85,3 +87,13 @@ def test_full_size_stripe_partition_equals_one_gpu(gpu, world):
         for blk in (render(scene, 2, 5, 8192, rank=r, world=world, stripe=STRIPE) for r in range(world))])
     full = rtamd.deinterleave(parts, 1080, world, STRIPE)
     assert bit_equal(full, one), mismatch_report(full, one)
+
+
+@pytest.mark.parametrize("sid", [8, 0])
+def test_ordered_chunks_equal_whole_launch_1080p(gpu, monkeypatch, sid):
+    """64 frames at 1080p as 64 one-frame chunks per tile (32 400 tiles, 63 wave-to-wave
+    hand-offs each, every chunk on whichever CU/XCD dequeues it) == one unit per tile."""
+    scene = rtamd.Scene(sid, 1920, 1080, seed=1)
+    whole = render(scene, 64, 5, 4096, chunk_target=0, monkeypatch=monkeypatch)
+    chunked = render(scene, 64, 5, 4096, chunk_target=100000, monkeypatch=monkeypatch)
+    assert bit_equal(chunked, whole), mismatch_report(chunked, whole)

@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--traffic-key", default="scene8_1920x1080_f64_d5")
     ap.add_argument("--traffic-out", default=os.path.join(REPO, "gpurun_out", "traffic.json"))
     ap.add_argument("--groups", default=None, help="comma list of group indices (default all)")
+    ap.add_argument("--valu-key", default=None, help="bench.py config key: write the roofline record to --valu-out")
+    ap.add_argument("--valu-out", default=os.path.join(REPO, "gpurun_out", "valu.json"))
+    ap.add_argument("--samples", type=int, default=1920 * 1080 * 64, help="samples in the profiled launch")
     a = ap.parse_args()
     listing = available() or ""
     res = {}
@@ -96,6 +99,22 @@ def main():
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
+    if a.valu_key and "SQ_INSTS_VALU" in res:
+        # the record bench.py's roofline reads (profiles/valu.json)
+        vj = {}
+        if os.path.exists(a.valu_out):
+            with open(a.valu_out) as f:
+                vj = json.load(f)
+        rec = {k: res[k] for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VALU_TRANS_F32", "valu_lane_utilization",
+                                   "hbm_bytes_per_launch", "hbm_read_bytes_x2", "hbm_write_bytes", "tcc_hit_rate")
+               if k in res}
+        rec["samples_per_launch"] = a.samples
+        rec["target"] = a.target
+        rec["method"] = ("rocprofv3 --kernel-trace --pmc, one counter group per pass, one render launch "
+                         "(tools/render_once.py); FETCH_SIZE x2 (gfx950) + WRITE_SIZE")
+        vj[a.valu_key] = rec
+        with open(a.valu_out, "w") as f:
+            json.dump(vj, f, indent=1, sort_keys=True)
     if a.traffic_key and "hbm_bytes_per_launch" in res:
         # the entry bench.py reads as roofline.traffic
         tj = {}

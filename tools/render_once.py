@@ -1,5 +1,5 @@
 """Minimal profiling target: render one batch of frames through rt.h and exit.
-usage: python tools/render_once.py [--scene 8] [--width 1920] [--height 1080] [--frames 64] [--launches 1]"""
+usage: python tools/render_once.py [--scene 8] [--width 1920] [--height 1080] [--frames 64] [--launches 1] [--spp 4096]"""
 import argparse
 import os
 import sys
@@ -15,11 +15,12 @@ ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--frames", type=int, default=64)
 ap.add_argument("--depth", type=int, default=5)
 ap.add_argument("--launches", type=int, default=1)
+ap.add_argument("--spp", type=int, default=4096, help="sqrt_spp uniform")
 a = ap.parse_args()
 scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
 ctx = rtamd.RenderContext(devices=(0,))
 ctx.upload_scene(scene)
-ctx.set_params(max_depth=a.depth, spp=4096)
+ctx.set_params(max_depth=a.depth, spp=a.spp)
 ctx.resize(a.width, a.height)
 f = 1
 for _ in range(a.launches):
