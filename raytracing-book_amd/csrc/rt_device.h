@@ -26,8 +26,9 @@
 #define RT_NODE_END 0xFFFFu
 #define RT_DFACE_F4 3    // float4 per dquads record
 #define RT_DBOX_F4 21    // float4 per dboxes record
-// LDS per 512-thread workgroup (2 workgroups per CU share 160 KiB): the static
-// running-mean slots (RT_LDS_ACC_BYTES) + the dynamic region (RT_LDS_DYN_BYTES)
+// LDS per 512-thread workgroup (2 workgroups per CU share 160 KiB): what the
+// launch shape stages (at most RT_LDS_DYN_BYTES), then the lanes' running-mean
+// slots (RT_LDS_ACC_BYTES), all in the dynamic region (no static LDS)
 #define RT_LDS_ACC_BYTES (512 * 16)
 #define RT_LDS_DYN_BYTES (80 * 1024 - RT_LDS_ACC_BYTES)   // link nodes + Perlin + media, or variant 61's tree + stacks
 #define RT_LDS_NODE_BYTES (64 * 1024)   // threaded (meta-word) nodes in LDS when they fit
@@ -98,6 +99,7 @@ struct rt_kernel_args {
     int n_media;
     int media_lds;               // float4 offset of the media records + sphere boundaries in LDS (3 float4
                                  // per medium, after the Perlin table), or -1
+    int acc_lds;                 // float4 offset of the lanes' running-mean slots (after everything staged)
     // exact near-first walk (variant 61; tables from rt_capi.hip build_fast)
     const uint32_t* finfo;       // per solid prim (finfo_base[type] + index): reference rank << 16 | reference leaf
     int fast_ok;
@@ -118,6 +120,6 @@ struct rt_kernel_args {
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves the default launch shape keeps resident on the current device
-int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream);
+int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream);   // sets a.acc_lds
 // debug: evaluate GLSL built-ins on device (tests)
 int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream);

@@ -425,13 +425,54 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
     }
 }
 
+// The link-format node loop from byte offset nx until a hit leaf or the end of
+// the walk (sign bit).  EXACT: the reference's per-axis slab (a -inf in 1/dir);
+// otherwise the NaN-ignoring min/max form.  The choice is wave-uniform and made
+// once per walk, outside the loop (3.6 % faster on scene 8 than testing it per
+// node step).  Reading both successors while the node is tested (to hide the
+// dependent LDS read) measured 9 % slower: the node loop is issue-bound.
+// Node reads: an LDS address is the node's byte offset plus the dynamic region's
+// base, which is 0 in a kernel without static LDS (every non-stats build), so
+// the offset is the address itself (no add per step).
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const f4v lds_f4;
+template <bool EXACT, bool STATS>
+__device__ __forceinline__ uint32_t link_walk(const char* __restrict__ base, uint32_t nx, v3 o, v3 inv, float tmin,
+                                              float tmax, unsigned long long* st) {
+    while ((int)nx >= 0) {
+        if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
+        float4 n0, n1;
+        if (STATS) {   // static LDS (the stats counters) precedes the dynamic region
+            n0 = *reinterpret_cast<const float4*>(base + nx);
+            n1 = *reinterpret_cast<const float4*>(base + nx + 16);
+        } else {
+            const lds_f4* p = (const lds_f4*)(uintptr_t)nx;
+            const f4v a = p[0], b = p[1];
+            n0 = make_float4(a.x, a.y, a.z, a.w);
+            n1 = make_float4(b.x, b.y, b.z, b.w);
+        }
+        bool hit;
+        if (!EXACT) {
+            hit = aabb_pk(n0, n1, o, inv, tmin, tmax);
+        } else {
+            float lo = tmin, hi = tmax;
+            slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+            slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+            slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+            hit = !(hi <= lo);
+        }
+        nx = __float_as_uint(hit ? n1.z : n1.w);
+    }
+    return nx;
+}
+
 // compute.glsl:226-266 over the threaded BVH.  Each lane's node sequence is the
 // reference's; only the interleaving of a wave's lanes differs: lanes advance
 // through inner/missed nodes until each holds a hit leaf (or is done), then the
 // leaves are tested together ("while-while").  LINK (variant 0/37): link-format
 // nodes; otherwise (variant 30) the threaded nodes with their meta word.  Both
 // use the branch-free node step with the NaN-exact min/max slab test.
-template <bool LINK, bool STATS>
+template <bool LINK, bool STATS, int OPT>
 __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ nodes, v3 o, v3 d, float time,
                                       float& rf, float px, float py, Hit& h, unsigned long long* st) {
     if (P.n_nodes == 0) return false;
@@ -452,22 +493,8 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
         uint32_t nx = 0u;
         for (;;) {
             unsigned long long t0 = STATS ? clock64() : 0;
-            while ((int)nx >= 0) {
-                if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-                const float4 n0 = *reinterpret_cast<const float4*>(base + nx);
-                const float4 n1 = *reinterpret_cast<const float4*>(base + nx + 16);
-                bool hitn;
-                if (!wave_exact) {
-                    hitn = aabb_pk(n0, n1, o, inv, tmin, tmax);
-                } else {
-                    float lo = tmin, hi = tmax;
-                    slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-                    slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-                    slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-                    hitn = !(hi <= lo);
-                }
-                nx = __float_as_uint(hitn ? n1.z : n1.w);
-            }
+            nx = wave_exact ? link_walk<true, STATS>(base, nx, o, inv, tmin, tmax, st)
+                            : link_walk<false, STATS>(base, nx, o, inv, tmin, tmax, st);
             if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
             if (nx == RT_LINK_END) break;
             unsigned long long t1 = STATS ? clock64() : 0;
@@ -1161,7 +1188,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 }
 
 // One iteration of ray_color's loop (compute.glsl:304-340).
-template <bool LINK, bool STATS, bool FAST>
+template <bool LINK, bool STATS, bool FAST, int OPT>
 __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, Path& S,
                                        float px, float py, v3& result, unsigned long long* st) {
     if (S.depth >= P.max_depth) {   // loop exhausted: final_color stays vec3(0)
@@ -1187,11 +1214,11 @@ __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ n
         } else {   // the exact walk, from the same rand() state
             unsigned long long c_ex = STATS ? clock64() : 0;
             S.rf = rf0;
-            hit = trace<LINK, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+            hit = trace<LINK, STATS, OPT>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
             if (STATS) st_add(st, ST_FAST_EXACT_CYC, clock64() - c_ex);
         }
     } else {
-        hit = trace<LINK, STATS>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
+        hit = trace<LINK, STATS, OPT>(P, nodes, S.o, d, S.time, S.rf, px, py, h, st);
     }
     unsigned long long ts = STATS ? clock64() : 0;
     if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
@@ -1257,7 +1284,7 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
 // costs spills at 128 VGPRs).  Path regeneration: a lane whose path ended
 // starts its next frame at once; each pixel still runs its frames in order, and
 // the mean is applied per frame in the reference's order.
-template <bool LINK, bool STATS, bool FAST>
+template <bool LINK, bool STATS, bool FAST, int OPT>
 __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, int x,
                                              int lr, int f0, int f1, float4* acc, unsigned long long* st) {
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
@@ -1279,7 +1306,7 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
             fresh = false;
         }
         v3 cur;
-        if (bounce<LINK, STATS, FAST>(P, nodes, fc, S, fx, fy, cur, st)) {
+        if (bounce<LINK, STATS, FAST, OPT>(P, nodes, fc, S, fx, fy, cur, st)) {
             int fc = P.first_frame + f;
             float n1 = (float)(fc - 1), n = (float)fc;
             float4 prev = *acc;
@@ -1342,11 +1369,10 @@ __device__ __forceinline__ void publish_chunk(const KP& P, int tile, int chunk) 
 //   LDSN: the nodes are staged in LDS (else read from global memory);
 //   FAST: the exact near-first stack walk (variant 61) with the reference walk
 //         as its fallback.
-template <bool LINK, int MINW, bool STATS, bool LDSN, int BLOCK, bool FAST>
+template <bool LINK, int MINW, bool STATS, bool LDSN, int BLOCK, bool FAST, int OPT = 0>
 __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __restrict__ Pp) {
     const KP& P = *Pp;
     extern __shared__ float4 s_nodes[];
-    __shared__ float4 s_acc[BLOCK];   // per lane: the pixel's running mean during a unit (RT_LDS_ACC_BYTES)
     __shared__ unsigned long long s_stats[STATS ? BLOCK / 64 : 1][STATS ? ST_N : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1403,6 +1429,9 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             }
         }
     }
+    // per lane: the pixel's running mean during a unit, after what this launch
+    // shape stages (P.acc_lds, set by rt_launch_render with the LDS size)
+    float4* s_acc = s_nodes + P.acc_lds;
     if (LDSN || STATS) __syncthreads();
     if (STATS) t_begin = clock64();
     const float4* __restrict__ rnodes = (LDSN && !FAST) ? s_nodes : reinterpret_cast<const float4*>(P.nodes);
@@ -1424,7 +1453,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         if (valid) {
             float4* px = reinterpret_cast<float4*>(P.image) + (size_t)lr * P.width + x;
             s_acc[tid] = *px;
-            render_pixel<LINK, STATS, FAST>(P, rnodes, fc, x, lr, f0, f1, s_acc + tid, st);
+            render_pixel<LINK, STATS, FAST, OPT>(P, rnodes, fc, x, lr, f0, f1, s_acc + tid, st);
             *px = s_acc[tid];
         }
         if (chunk + 1 < P.n_chunks) publish_chunk(P, tile, chunk);
@@ -1482,13 +1511,51 @@ int rt_resident_waves(void) {
     return cus * 2 * (512 / 64);   // default shape: 2 workgroups of 512 per CU
 }
 
-int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
+int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    // Variants (RT_KERNEL_VARIANT; all bit-identical, tests/test_gpu_boundary.py):
+    //   0 = 37: link-format nodes in LDS (+ the Perlin table and media records), 512 threads,
+    //           4 waves per SIMD; 38 its stats twin.  Falls back to 30 when the link format is
+    //           unavailable (> 2047 nodes) or does not fit LDS.
+    //   30: threaded nodes with the meta word (in LDS when they fit, else global); 31 stats twin.
+    //   61: the exact near-first stack walk (tree and stacks in LDS); 69 stats twin.
+    // Every shape's dynamic LDS ends with the lanes' running-mean slots (RT_LDS_ACC_BYTES).
+    const size_t lds_t = (size_t)a.n_nodes * sizeof(rt_dnode);   // threaded nodes
+    const bool fits_t = lds_t <= RT_LDS_NODE_BYTES;
+    // after the nodes, as placed by the host: the Perlin table, then the media records
+    const size_t extra_end =
+        a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
+        : a.perlin_lds >= 0 ? ((size_t)a.perlin_lds + ((size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h + 3) / 4) * 16
+                            : 0;
+    const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
+    const size_t lds_p = lds_t > extra_end ? lds_t : extra_end;
+    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69;
+    const size_t acc = RT_LDS_ACC_BYTES;
+    // the launch shape and its staged bytes (before the running-mean slots)
+    enum { FAST_LDS, FAST_GLOBAL, LINK_LDS, META_LDS, META_GLOBAL } shape;
+    size_t staged;
+    const size_t stack_b = (size_t)RT_FAST_STACK * 512 * sizeof(short);
+    const size_t tree_b = (size_t)a.n_f2inner * 64 + (size_t)((a.n_f2leaves + 1) / 2) * 16;
+    if (a.variant == 61 || a.variant == 69) {
+        shape = tree_b + stack_b <= RT_LDS_DYN_BYTES ? FAST_LDS : FAST_GLOBAL;
+        staged = shape == FAST_LDS ? tree_b + stack_b : stack_b;
+    } else if (a.variant != 30 && a.variant != 31 && a.n_lnode_f4 > 0 && lds_l <= RT_LDS_DYN_BYTES) {
+        shape = LINK_LDS;
+        staged = lds_l;
+    } else if (fits_t && lds_p <= RT_LDS_DYN_BYTES) {
+        shape = META_LDS;
+        staged = lds_p;
+    } else {
+        shape = META_GLOBAL;
+        staged = 0;
+    }
+    a.acc_lds = (int)(staged / 16);
+    const size_t lds = staged + acc;
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.
     // `a` is a pinned staging slot; same-stream ordering makes one device slot
     // safe to reuse per launch.
-    hipStream_t st = (hipStream_t)stream;
     if (hipMemcpyAsync(dargs, &a, sizeof(a), hipMemcpyHostToDevice, st) != hipSuccess) return -1;
     const rt_kernel_args* d = (const rt_kernel_args*)dargs;
     // the work-unit counter, then (ordered chunks) the tiles' published chunk counts
@@ -1496,41 +1563,28 @@ int rt_launch_render(const rt_kernel_args& a, rt_kernel_args* dargs, void* strea
     if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
     if (a.n_chunks > 1 && hipMemsetAsync(a.tile_done, 0, sizeof(unsigned) * (size_t)n_tiles, st) != hipSuccess)
         return -1;
-    // Variants (RT_KERNEL_VARIANT; all bit-identical, tests/test_gpu_boundary.py):
-    //   0 = 37: link-format nodes in LDS (+ the Perlin table and media records), 512 threads,
-    //           4 waves per SIMD; 38 its stats twin.  Falls back to 30 when the link format is
-    //           unavailable (> 2047 nodes) or does not fit LDS.
-    //   30: threaded nodes with the meta word (in LDS when they fit, else global); 31 stats twin.
-    //   61: the exact near-first stack walk (tree and stacks in LDS); 69 stats twin.
-    const size_t lds_t = (size_t)a.n_nodes * sizeof(rt_dnode);   // threaded nodes
-    const bool fits_t = lds_t <= RT_LDS_NODE_BYTES;
-    // after the nodes, as placed by the host: the Perlin table, then the media records
-    const size_t extra_end = a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
-                             : a.perlin_lds >= 0
-                                 ? ((size_t)a.perlin_lds + (size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h / 4) * 16
-                                 : 0;
-    const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
-    const size_t lds_p = lds_t > extra_end ? lds_t : extra_end;
-    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69;
     int rc;
-    if (a.variant == 61 || a.variant == 69) {
-        const size_t stack_b = (size_t)RT_FAST_STACK * 512 * sizeof(short);
-        const size_t tree_b = (size_t)a.n_f2inner * 64 + (size_t)((a.n_f2leaves + 1) / 2) * 16;
-        const bool in_lds = tree_b + stack_b <= RT_LDS_DYN_BYTES;
-        const size_t l2 = in_lds ? tree_b + stack_b : stack_b;
-        if (stats) rc = in_lds ? launch_persistent(render_persistent<false, 4, true, true, 512, true>, 512, l2, d, st)
-                               : launch_persistent(render_persistent<false, 4, true, false, 512, true>, 512, l2, d, st);
-        else rc = in_lds ? launch_persistent(render_persistent<false, 4, false, true, 512, true>, 512, l2, d, st)
-                         : launch_persistent(render_persistent<false, 4, false, false, 512, true>, 512, l2, d, st);
-    } else if (a.variant != 30 && a.variant != 31 && a.n_lnode_f4 > 0 && lds_l <= RT_LDS_DYN_BYTES) {
-        rc = stats ? launch_persistent(render_persistent<true, 4, true, true, 512, false>, 512, lds_l, d, st)
-                   : launch_persistent(render_persistent<true, 4, false, true, 512, false>, 512, lds_l, d, st);
-    } else if (fits_t && lds_p <= RT_LDS_DYN_BYTES) {
-        rc = stats ? launch_persistent(render_persistent<false, 4, true, true, 512, false>, 512, lds_p, d, st)
-                   : launch_persistent(render_persistent<false, 4, false, true, 512, false>, 512, lds_p, d, st);
-    } else {
-        rc = stats ? launch_persistent(render_persistent<false, 4, true, false, 512, false>, 512, 0, d, st)
-                   : launch_persistent(render_persistent<false, 4, false, false, 512, false>, 512, 0, d, st);
+    switch (shape) {
+        case FAST_LDS:
+            rc = stats ? launch_persistent(render_persistent<false, 4, true, true, 512, true>, 512, lds, d, st)
+                       : launch_persistent(render_persistent<false, 4, false, true, 512, true>, 512, lds, d, st);
+            break;
+        case FAST_GLOBAL:
+            rc = stats ? launch_persistent(render_persistent<false, 4, true, false, 512, true>, 512, lds, d, st)
+                       : launch_persistent(render_persistent<false, 4, false, false, 512, true>, 512, lds, d, st);
+            break;
+        case LINK_LDS:
+            rc = stats ? launch_persistent(render_persistent<true, 4, true, true, 512, false>, 512, lds, d, st)
+                       : launch_persistent(render_persistent<true, 4, false, true, 512, false>, 512, lds, d, st);
+            break;
+        case META_LDS:
+            rc = stats ? launch_persistent(render_persistent<false, 4, true, true, 512, false>, 512, lds, d, st)
+                       : launch_persistent(render_persistent<false, 4, false, true, 512, false>, 512, lds, d, st);
+            break;
+        default:
+            rc = stats ? launch_persistent(render_persistent<false, 4, true, false, 512, false>, 512, lds, d, st)
+                       : launch_persistent(render_persistent<false, 4, false, false, 512, false>, 512, lds, d, st);
+            break;
     }
     if (rc) return rc;
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -144,3 +144,21 @@ def test_scene8_earth_texture_pattern_matches_gallery():
         return v - X @ coef
     corr = [float(np.corrcoef(resid(ours[:, c]), resid(gal[:, c]))[0, 1]) for c in range(3)]
     assert min(corr) >= EARTH_MIN_CORR, corr
+
+
+@pytest.mark.gpu
+def test_scene0_sky_through_the_kernel(gpu, scene0_top):
+    """The same sky rows rendered by the HIP kernel through rt.h: the bits of the oracle's
+    rows, hence the gallery's sky bytes."""
+    sc, ref = scene0_top
+    ctx = rtamd.RenderContext(devices=(0,))
+    ctx.upload_scene(sc)
+    ctx.set_params(max_depth=5, spp=64)
+    ctx.resize(sc.width, sc.height)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 64))
+    out = ctx.read_image()[:ref.shape[0]]
+    ctx.close()
+    from helpers import bit_equal, mismatch_report
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+    full = FIX["scene0_sky"]["full_rows"]
+    assert (rtamd.tonemap_rgb8(out[:full]) == np.array(FIX["scene0_sky"]["rgb"], np.uint8)).all()
