@@ -23,6 +23,9 @@
 // rand() consumption order is identical to the reference.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "rt/rt_glsl.h"
 #include "rt_device.h"
 
@@ -46,7 +49,10 @@ enum {
     // near-first walk (variants 60/61): traces, those that took the exact walk (and why: 9 reasons),
     // node steps and prim tests
     ST_FAST_TRACES, ST_FAST_EXACT, ST_FAST_WHY, ST_FAST_STEPS = ST_FAST_WHY + 9, ST_FAST_TESTS,
-    ST_FAST_PRE_CYC, ST_FAST_POST_CYC, ST_FAST_EXACT_CYC, ST_N
+    ST_FAST_PRE_CYC, ST_FAST_POST_CYC, ST_FAST_EXACT_CYC,
+    // leaf stage by prim type: wave-cycles from the slot's start to the end of that type's test
+    // (the types run one after another in this order, so each includes the ones before it)
+    ST_SPH_CYC, ST_QUAD_CYC, ST_BOX_CYC, ST_MED_CYC, ST_N
 };
 __device__ __forceinline__ bool first_active_lane() {
     unsigned long long m = __ballot(1);
@@ -403,19 +409,24 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
         float t = 0.0f, al = 0.0f, be = 0.0f;
         int face = 0;
         bool hit = false;
+        unsigned long long c0 = STATS ? clock64() : 0;
         if (ty == RT_MODEL_SPHERE) {
             hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t);
             if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
+            if (STATS) st_add(st, ST_SPH_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_QUAD) {
             hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, tmax, t, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
+            if (STATS) st_add(st, ST_QUAD_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_BOX) {
             hit = (P.boxes_canon && fin) ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix + 18, P.dboxes + RT_DBOX_F4 * ix, o,
                                                           d, tmin, tmax, t, face, al, be)
                                          : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
+            if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
             hit = medium_test(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
+            if (STATS) st_add(st, ST_MED_CYC, clock64() - c0);
         }
         if (hit) {
             has = true;
@@ -1552,6 +1563,11 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     }
     a.acc_lds = (int)(staged / 16);
     const size_t lds = staged + acc;
+    static const bool log_shape = std::getenv("RT_LOG_SHAPE") != nullptr;   // diagnostics: the chosen launch shape
+    if (log_shape)
+        std::fprintf(stderr, "rt_launch_render: shape %d (0 fast-lds 1 fast-global 2 link 3 meta-lds 4 meta-global), "
+                             "lds %zu B, media_lds %d, perlin_lds %d, chunks %d\n",
+                     (int)shape, lds, a.media_lds, a.perlin_lds, a.n_chunks);
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.
     // `a` is a pinned staging slot; same-stream ordering makes one device slot

@@ -140,12 +140,15 @@ def test_bound_torch_image_and_stream(gpu):
 VARIANTS = [0, 30, 61]   # link-format walk (default), threaded meta walk, exact near-first walk
 
 
+@pytest.mark.parametrize("sid", [8, 6, 7])
 @pytest.mark.parametrize("chunk_target", ["0", "1", "16", "100000"])
-def test_all_kernel_variants_identical(gpu, monkeypatch, chunk_target):
+def test_all_kernel_variants_identical(gpu, monkeypatch, chunk_target, sid):
     """Every launch shape of the kernel (RT_KERNEL_VARIANT) and every work split
     (RT_CHUNK_TARGET: 0 = one unit per tile with all frames, else tile x ordered
-    frame-chunk units handed over between waves) renders the same bits."""
-    s = rtamd.Scene(8, 40, 24, seed=1)
+    frame-chunk units handed over between waves) renders the same bits; scenes 8
+    (canonical boxes, media, Perlin, image texture), 6 and 7 (rotated boxes: the
+    general box test)."""
+    s = rtamd.Scene(sid, 40, 24, seed=1)
     ref = oracle_image(s, 6)
     monkeypatch.setenv("RT_CHUNK_TARGET", chunk_target)
     for v in VARIANTS:

@@ -2,9 +2,9 @@
 
 Every variant must produce the same bits; timings are HIP-event device time of
 one rt_render call (1 launch) per round, reported as median/min over rounds.
-A variant spec is "<RT_KERNEL_VARIANT>" optionally followed by c<RT_CHUNK_TARGET>
-and/or k<RT_SHADE_K> and/or d<RT_DEBUG_FLAGS> (ablations: bits differ by design) (e.g. 30c0 = variant 30 with the direct, unchunked work
-split; 42k16 = variant 42 shading once 16 lanes wait).
+A variant spec is "<RT_KERNEL_VARIANT>" optionally followed by c<RT_CHUNK_TARGET>,
+k<RT_SHADE_K> and/or d<RT_DEBUG_FLAGS> (ablations: bits differ by design) (e.g.
+30c0 = variant 30 with one unit per tile).
 usage: python tools/ab_variants.py [--variants 30c0,30c16] [--rounds 5] [--scene 8]
 """
 import argparse

@@ -13,7 +13,8 @@ import rtamd  # noqa: E402
 NAMES = ["TOTAL", "START_CYC", "START_IT", "START_LN", "NODE_CYC", "NODE_IT", "NODE_LN", "LEAF_CYC", "LEAF_IT",
          "LEAF_LN", "SPH_LN", "QUAD_LN", "BOX_LN", "MED_LN", "SHADE_CYC", "SHADE_IT", "SHADE_LN", "SPH_IT",
          "QUAD_IT", "BOX_IT", "MED_IT", "FAST_TRACES", "FAST_EXACT"] + [f"FAST_WHY{r}" for r in range(1, 10)] + [
-         "FAST_STEPS", "FAST_TESTS", "FAST_PRE_CYC", "FAST_POST_CYC", "FAST_EXACT_CYC"]
+         "FAST_STEPS", "FAST_TESTS", "FAST_PRE_CYC", "FAST_POST_CYC", "FAST_EXACT_CYC",
+         "SPH_CYC", "QUAD_CYC", "BOX_CYC", "MED_CYC"]
 
 
 def main():
@@ -46,7 +47,9 @@ def main():
               f"cyc/iter {cyc / max(it, 1):7.1f}  lane-iters/sample {ln / samples:6.2f}")
     for t in ["SPH", "QUAD", "BOX", "MED"]:
         it, ln = v[t + "_IT"], v[t + "_LN"]
-        print(f"  leaf-slot {t:4s}: wave-executions {it:.3e} lanes/exec {ln / max(it, 1):5.2f}  per-sample {ln / samples:5.2f}")
+        cyc = v[t + "_CYC"]
+        print(f"  leaf-slot {t:4s}: wave-executions {it:.3e} lanes/exec {ln / max(it, 1):5.2f}  per-sample {ln / samples:5.2f}"
+              f"  {100.0 * cyc / tot:5.1f}% of wave-cycles  cyc/exec {cyc / max(it, 1):7.1f}")
     print("raw", v)
 
 

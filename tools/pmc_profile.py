@@ -31,6 +31,10 @@ GROUPS = [
      "SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL"],
     ["TCP_PENDING_STALL_CYCLES_sum", "TCP_TCR_RDRET_STALL_sum", "TCP_READ_TAGCONFLICT_STALL_CYCLES_sum",
      "TCP_TCP_TA_DATA_STALL_CYCLES_sum"],
+    # 14, 15: instruction fetch (SQC instruction cache) and where wave time goes
+    ["SQC_ICACHE_HITS", "SQC_ICACHE_MISSES", "SQC_ICACHE_MISSES_DUPLICATE", "SQC_ICACHE_REQ"],
+    ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_IFETCH", "SQ_IFETCH_LEVEL",
+     "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA"],
 ]
 
 
