@@ -42,6 +42,8 @@ struct Device {
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
     DevBuf counter;          // persistent-kernel work-unit counter [0] and fault word [1]
     DevBuf tile_done;        // ordered chunks: chunks published per 8x8 tile
+    DevBuf samples;          // staged chunks: per-frame colours [frames][local pixels]
+    DevBuf wbuf;             // pooled units (ordered / one chunk): per resident wave 64 x chunk_frames colours
     DevBuf finfo;            // exact near-first walk tables (variant 61)
     DevBuf f2inner, f2leaves;
     DevBuf links;            // link-format BVH (variant 0/37)
@@ -103,9 +105,15 @@ struct rt_ctx {
     int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
     int variant_no_stats = -1;   // the variant active before rt_debug_enable_stats(c, 1), restored by (c, 0)
     // Work split: aim for chunk_target work units per resident wave (env
-    // RT_CHUNK_TARGET; 0 = one chunk per tile).  A launch over few tiles per wave
-    // splits its frames into ordered chunks (rt_kernel.hip wait_chunk).
+    // RT_CHUNK_TARGET; 0 = one chunk per tile).  With at least stage_tiles tiles
+    // per resident wave (env RT_STAGE_TILES) the chunks are ordered (the running
+    // mean is handed from wave to wave, rt_kernel.hip wait_chunk); with fewer, a
+    // tile's frames would be one long serial chain, so the chunks run in parallel,
+    // stage their per-frame colours (at most sample_budget bytes) and fold_kernel
+    // applies the running mean in frame order.
     int chunk_target = 32;
+    int stage_tiles = 4;
+    size_t sample_budget = (size_t)16 << 30;
 };
 
 namespace {
@@ -701,9 +709,12 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) {
         // 0 = 37 (default), 30, 61 and their stats twins 38, 31, 69; anything else is the default
         const int want = std::atoi(v);
-        c->variant = (want == 30 || want == 31 || want == 37 || want == 38 || want == 61 || want == 69) ? want : 0;
+        c->variant = (want == 30 || want == 31 || want == 37 || want == 38 || want == 39 || want == 61 || want == 69)
+                         ? want
+                         : 0;
     }
     if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("RT_STAGE_TILES")) c->stage_tiles = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
@@ -730,7 +741,7 @@ int rt_destroy(rt_ctx* c) {
         (void)hipStreamSynchronize(d.stream);
         dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter);
-        dev_free(d.tile_done); dev_free(d.dquads); dev_free(d.dboxes);
+        dev_free(d.tile_done); dev_free(d.samples); dev_free(d.wbuf); dev_free(d.dquads); dev_free(d.dboxes);
         dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
@@ -1062,14 +1073,35 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         // are split into ordered chunks so the dynamic schedule has enough units
         // to balance (rt_kernel.hip wait_chunk / publish_chunk).
         const int n_tiles = ((c->width + 7) / 8) * ((d.local_rows + 7) / 8);
-        const int per_launch = RT_MAX_FRAMES_PER_LAUNCH;
+        int per_launch = RT_MAX_FRAMES_PER_LAUNCH;
         int chunks_wanted = 1;
+        const long long waves = rt_resident_waves();
         if (c->chunk_target > 0 && n_tiles > 0) {
-            long long waves = rt_resident_waves();
             chunks_wanted = (int)std::min<long long>(RT_MAX_FRAMES_PER_LAUNCH,
                                                      (c->chunk_target * waves + n_tiles - 1) / n_tiles);
         }
-        if (chunks_wanted > 1 && d.tile_done.bytes < sizeof(unsigned) * (size_t)n_tiles) {
+        const bool staged = chunks_wanted > 1 && (long long)n_tiles < (long long)c->stage_tiles * waves;
+        const size_t n_pixels = (size_t)d.local_rows * c->width;
+        if (staged) {
+            const size_t per_frame = n_pixels * sizeof(float4);
+            per_launch = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, c->sample_budget / per_frame));
+        }
+        {   // equal launches: no short last launch that the whole grid waits on
+            const int n_launch = (std::max(n_frames, 1) + per_launch - 1) / per_launch;
+            per_launch = (std::max(n_frames, 1) + n_launch - 1) / n_launch;
+        }
+        if (staged) {
+            const size_t per_frame = n_pixels * sizeof(float4);
+            const size_t need = per_frame * (size_t)std::min(per_launch, std::max(n_frames, 1));
+            if (d.samples.bytes < need) {
+                dev_free(d.samples);
+                HIPCHK(c, hipMalloc(&d.samples.ptr, need));
+                d.samples.bytes = need;
+            }
+        }
+        a.samples = staged ? (float4*)d.samples.ptr : nullptr;
+        a.n_pixels = n_pixels;
+        if (!staged && chunks_wanted > 1 && d.tile_done.bytes < sizeof(unsigned) * (size_t)n_tiles) {
             dev_free(d.tile_done);
             HIPCHK(c, hipMalloc(&d.tile_done.ptr, sizeof(unsigned) * (size_t)n_tiles));
             d.tile_done.bytes = sizeof(unsigned) * (size_t)n_tiles;
@@ -1084,6 +1116,20 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             a.n_chunks = std::max(1, std::min(chunks_wanted, nf));
             a.chunk_frames = (nf + a.n_chunks - 1) / a.n_chunks;
             a.n_chunks = (nf + a.chunk_frames - 1) / a.chunk_frames;
+            if (a.n_chunks == 1) a.samples = nullptr;   // one chunk: the running mean in place
+            else if (staged) a.samples = (float4*)d.samples.ptr;
+            a.wbuf = nullptr;
+            a.wbuf_waves = 0;
+            if (!a.samples && (c->variant == 0 || c->variant == 39)) {   // pooled units fold per wave
+                const size_t need = (size_t)waves * 64 * (size_t)a.chunk_frames * sizeof(float4);
+                if (d.wbuf.bytes < need) {
+                    dev_free(d.wbuf);
+                    HIPCHK(c, hipMalloc(&d.wbuf.ptr, need));
+                    d.wbuf.bytes = need;
+                }
+                a.wbuf = (float4*)d.wbuf.ptr;
+                a.wbuf_waves = (int)waves;
+            }
             std::memcpy(a.rand_factors, rand_factors + f0, sizeof(float) * nf);
             int slot = d.ring_pos++ % Device::kRing;
             HIPCHK(c, hipEventSynchronize(d.ring_ev[slot]));   // the copy that last used this slot is done
@@ -1285,11 +1331,12 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
     return (F.ok && boxes_nest(dn)) ? 1 : 0;
 }
 
-// The stats twin (region timers + lane counters) of a launch variant: 61 -> 69, 30 -> 31, 0/37 -> 38.
+// The stats twin (region timers + lane counters) of a launch variant: 61 -> 69, 30 -> 31, 37 -> 38, 0 -> 39.
 static int stats_twin(int v) {
     if (v == 61 || v == 69) return 69;
     if (v == 30 || v == 31) return 31;
-    return 38;
+    if (v == 37 || v == 38) return 38;
+    return 39;
 }
 
 int rt_debug_enable_stats(rt_ctx* c, int on) {
@@ -1304,7 +1351,6 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
         if (d.stats.ptr) HIPCHK(c, hipMemsetAsync(d.stats.ptr, 0, d.stats.bytes, d.stream));
         HIPCHK(c, hipStreamSynchronize(d.stream));
     }
-    // stats twin of the current launch shape: 12/15/30 -> 31, 10 -> 19, 0/37 -> 38
     if (on) {
         if (c->variant_no_stats < 0) c->variant_no_stats = c->variant;
         c->variant = stats_twin(c->variant_no_stats);

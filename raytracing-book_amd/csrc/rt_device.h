@@ -15,6 +15,9 @@
 //   textures : RGB8 expanded to RGBA8 (4 B/texel, aligned), RGBA8, R32F
 //   image    : float4 [padded_local_rows][W], stripe-compacted rows
 //   tile_done: uint32 [tiles] chunks published per 8x8 tile (ordered-chunk launches)
+//   samples  : float4 [frames][local_rows*W] per-frame colours (staged-chunk launches)
+//   wbuf     : float4 [resident waves][chunk_frames][64] per-wave sample colours of the
+//              unit in flight (pooled units, ordered / one-chunk launches)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -90,7 +93,11 @@ struct rt_kernel_args {
     // work split: unit = chunk * n_tiles + tile, chunk = frames [c*chunk_frames, ...) (ordered chunks)
     int n_chunks, chunk_frames;
     unsigned* tile_done;         // ordered chunks: per tile, the chunks published so far (zeroed per launch)
+    float4* samples;             // staged chunks: per-frame colours [n_frames][n_pixels]; nullptr = ordered / one chunk
+    size_t n_pixels;             // local_rows * width
     unsigned* fault;             // set when an ordered-chunk wait times out (rt_sync reports it)
+    float4* wbuf;                // pooled units, ordered / one chunk: per resident wave 64 * chunk_frames colours
+    int wbuf_waves;              // waves wbuf has slots for (the launch's grid never exceeds it)
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
@@ -119,7 +126,7 @@ struct rt_kernel_args {
 };
 
 // launcher implemented in rt_kernel.hip
-int rt_resident_waves(void);   // waves the default launch shape keeps resident on the current device
+int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)
 int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream);   // sets a.acc_lds
 // debug: evaluate GLSL built-ins on device (tests)
 int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream);

@@ -5,11 +5,14 @@
 // oracle given the shared GLSL built-in definitions (include/rt/rt_glsl.h) and
 // -ffp-contract=off.  Structure (MI355X-first; every change value-preserving):
 //   * persistent grid: each workgroup stages the threaded BVH in LDS once and
-//     each wave pulls 8x8 pixel tiles from a device-wide counter;
-//   * a work-item owns one pixel and loops over ALL frames of the launch with
-//     path regeneration (a finished path starts the pixel's next frame at
-//     once); the RGBA32F running mean (compute.glsl:355) is applied per frame
-//     exactly, but the image is read/written once per launch;
+//     each wave pulls units (8x8 pixel tile x a chunk of the launch's frames)
+//     from a device-wide counter;
+//   * the wave's lanes share the unit's samples (render_pool): a lane whose
+//     path ended takes the next unclaimed (pixel, frame); the colours are
+//     folded into the RGBA32F running mean (compute.glsl:355) per pixel in
+//     frame order at the end of the unit, so the image is read/written once
+//     per unit (variant 37: a lane owns one pixel and regenerates only its own
+//     frames);
 //   * stackless walk of a threaded BVH (rt_dnode) visiting the reference's node
 //     sequence (stack pops, right child first) without the int stack[64];
 //   * lean hit record during the walk (t, type, index, box face, uv source);
@@ -32,6 +35,9 @@
 namespace {
 
 typedef rt_kernel_args KP;
+
+// OPT bits of the kernel templates
+#define RT_OPT_POOL 1   // pooled units (render_pool): the default; without it a lane owns a pixel (variant 37)
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -1298,6 +1304,7 @@ __device__ __forceinline__ void start_path(const KP& P, Path& S, int frame_count
 template <bool LINK, bool STATS, bool FAST, int OPT>
 __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, int x,
                                              int lr, int f0, int f1, float4* acc, unsigned long long* st) {
+    const uint32_t pix = (uint32_t)lr * (uint32_t)P.width + (uint32_t)x;   // local pixel index (staged chunks)
     int gstripe = (lr / P.stripe_rows) * P.world + P.rank;
     int y = gstripe * P.stripe_rows + lr % P.stripe_rows;
     const rt_camera_ubo& C = P.cam;
@@ -1318,15 +1325,77 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
         }
         v3 cur;
         if (bounce<LINK, STATS, FAST, OPT>(P, nodes, fc, S, fx, fy, cur, st)) {
-            int fc = P.first_frame + f;
-            float n1 = (float)(fc - 1), n = (float)fc;
-            float4 prev = *acc;
-            prev.x = (prev.x * n1 + cur.x) / n;
-            prev.y = (prev.y * n1 + cur.y) / n;
-            prev.z = (prev.z * n1 + cur.z) / n;
-            prev.w = 1.0f;
-            *acc = prev;
+            if (P.samples) {   // staged chunks: fold_kernel applies the running mean in frame order
+                P.samples[(size_t)f * P.n_pixels + pix] = make_float4(cur.x, cur.y, cur.z, 0.0f);
+            } else {
+                int fc = P.first_frame + f;
+                float n1 = (float)(fc - 1), n = (float)fc;
+                float4 prev = *acc;
+                prev.x = (prev.x * n1 + cur.x) / n;
+                prev.y = (prev.y * n1 + cur.y) / n;
+                prev.z = (prev.z * n1 + cur.z) / n;
+                prev.w = 1.0f;
+                *acc = prev;
+            }
             f++;
+            fresh = true;
+        }
+    }
+}
+
+// Pooled unit (variant 0): the wave's 64 lanes share the unit's samples -- the
+// tile's nv valid pixels x its kf frames, sample s = frame-in-chunk * nv + pixel
+// -- instead of each lane owning one pixel.  A lane whose path ends takes the
+// next unclaimed sample (one ballot per loop iteration: the lanes needing work
+// get consecutive indices by mbcnt), so no lane idles while the wave still has
+// samples, whichever pixels' paths run long.  A sample's bits depend only on
+// its pixel and frame (random.glsl:2-7), not on the lane that runs it.  Colours
+// go to `out` by (frame-in-chunk, pixel slot = py * 8 + px): the unit's per-wave
+// slot (ordered / one chunk; the caller folds them in frame order) or, for
+// staged chunks, straight to P.samples.
+template <bool LINK, bool STATS, bool FAST, int OPT>
+__device__ __forceinline__ void render_pool(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc,
+                                            int tx0, int ly0, int wt, int ht, int f0, int kf, float4* wslot,
+                                            unsigned long long* st) {
+    const uint32_t nv = (uint32_t)(wt * ht), total = nv * (uint32_t)kf;
+    const rt_camera_ubo& C = P.cam;
+    uint32_t next = 0;   // first unclaimed sample (the same in every lane)
+    uint32_t s = 0;
+    float fx = 0.0f, fy = 0.0f;
+    Path S;
+    bool fresh = true;
+    for (;;) {
+        const unsigned long long need = __ballot(fresh);
+        if (fresh)
+            s = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        next += (uint32_t)__popcll(need);
+        if (fresh) {
+            if (s >= total) break;
+            const uint32_t fl = s / nv, p = s - fl * nv;
+            const int lr = ly0 + (int)(p / (uint32_t)wt), x = tx0 + (int)(p % (uint32_t)wt);
+            const int y = ((lr / P.stripe_rows) * P.world + P.rank) * P.stripe_rows + lr % P.stripe_rows;
+            fx = (float)x;
+            fy = (float)y;
+            unsigned long long t0 = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
+            // get_norm_coord (compute.glsl:268-283) before its jitter term
+            const v3 base =
+                add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)), scale3(ld3(C.pixel_delta_v), fy));
+            const int f = f0 + (int)fl;
+            start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, base);
+            if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
+            fresh = false;
+        }
+        v3 cur;
+        if (bounce<LINK, STATS, FAST, OPT>(P, nodes, fc, S, fx, fy, cur, st)) {
+            const uint32_t fl = s / nv, p = s - fl * nv;
+            const uint32_t py = p / (uint32_t)wt, px = p - py * (uint32_t)wt;
+            const float4 c4 = make_float4(cur.x, cur.y, cur.z, 0.0f);
+            if (wslot)
+                wslot[fl * 64u + py * 8u + px] = c4;
+            else
+                P.samples[(size_t)(f0 + (int)fl) * P.n_pixels + (uint32_t)(ly0 + (int)py) * (uint32_t)P.width +
+                          (uint32_t)(tx0 + (int)px)] = c4;
             fresh = true;
         }
     }
@@ -1460,14 +1529,43 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         const int x = (tile % tiles_x) * 8 + (lane & 7);
         const int lr = (tile / tiles_x) * 8 + (lane >> 3);
         const bool valid = x < P.width && lr < P.local_rows;   // lane 0 (the tile's corner) always is
-        if (chunk > 0) wait_chunk(P, tile, chunk);
+        const bool ordered = P.samples == nullptr;             // else staged: chunks independent
+        if (OPT & RT_OPT_POOL) {
+            const int tx0 = x - (lane & 7), ly0 = lr - (lane >> 3);
+            float4* wslot =
+                ordered ? P.wbuf + ((size_t)blockIdx.x * (BLOCK / 64) + (tid >> 6)) * 64 * P.chunk_frames : nullptr;
+            render_pool<LINK, STATS, FAST, OPT>(P, rnodes, fc, tx0, ly0, min(8, P.width - tx0),
+                                                min(8, P.local_rows - ly0), f0, f1 - f0, wslot, st);
+            if (!ordered) continue;
+            // the unit's colours, written by any lane of this wave, folded by the pixel's lane
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (chunk > 0) wait_chunk(P, tile, chunk);
+            if (valid) {
+                float4* px = reinterpret_cast<float4*>(P.image) + (size_t)lr * P.width + x;
+                float4 prev = *px;
+                for (int f = f0; f < f1; f++) {
+                    const float4 cur = wslot[(f - f0) * 64 + lane];
+                    const int fcnt = P.first_frame + f;
+                    const float n1 = (float)(fcnt - 1), n = (float)fcnt;
+                    prev.x = (prev.x * n1 + cur.x) / n;
+                    prev.y = (prev.y * n1 + cur.y) / n;
+                    prev.z = (prev.z * n1 + cur.z) / n;
+                    prev.w = 1.0f;
+                }
+                *px = prev;
+            }
+            if (chunk + 1 < P.n_chunks) publish_chunk(P, tile, chunk);
+            continue;
+        }
+        if (ordered && chunk > 0) wait_chunk(P, tile, chunk);
         if (valid) {
             float4* px = reinterpret_cast<float4*>(P.image) + (size_t)lr * P.width + x;
-            s_acc[tid] = *px;
+            if (ordered) s_acc[tid] = *px;
             render_pixel<LINK, STATS, FAST, OPT>(P, rnodes, fc, x, lr, f0, f1, s_acc + tid, st);
-            *px = s_acc[tid];
+            if (ordered) *px = s_acc[tid];
         }
-        if (chunk + 1 < P.n_chunks) publish_chunk(P, tile, chunk);
+        if (ordered && chunk + 1 < P.n_chunks) publish_chunk(P, tile, chunk);
     }
     if (STATS) {
         st_add(st, ST_TOTAL, clock64() - t_begin);
@@ -1478,6 +1576,28 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             atomicAdd(P.stats + tid, v);
         }
     }
+}
+
+// Staged-chunk epilogue: the running mean of compute.glsl:355 over the launch's
+// frames, in frame order, per pixel: (prev*(n-1)+cur)/n -- the operations the
+// ordered path applies in LDS, so the same bits.
+__global__ void __launch_bounds__(256) fold_kernel(const KP* __restrict__ Pp) {
+    const KP& P = *Pp;
+    const size_t pix = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (pix >= P.n_pixels) return;
+    float4* px = reinterpret_cast<float4*>(P.image) + pix;
+    float4 prev = *px;
+    const float4* s = P.samples + pix;
+    for (int f = 0; f < P.n_frames; f++) {
+        const float4 cur = s[(size_t)f * P.n_pixels];
+        const int fc = P.first_frame + f;
+        const float n1 = (float)(fc - 1), n = (float)fc;
+        prev.x = (prev.x * n1 + cur.x) / n;
+        prev.y = (prev.y * n1 + cur.y) / n;
+        prev.z = (prev.z * n1 + cur.z) / n;
+        prev.w = 1.0f;
+    }
+    *px = prev;
 }
 
 __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const float* __restrict__ y,
@@ -1499,7 +1619,8 @@ __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const f
 }
 
 template <typename K>
-int launch_persistent(K kernel, int block, size_t lds, const rt_kernel_args* d, hipStream_t st) {
+int launch_persistent(K kernel, int block, size_t lds, const rt_kernel_args& a, const rt_kernel_args* d,
+                      hipStream_t st) {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
@@ -1509,6 +1630,9 @@ int launch_persistent(K kernel, int block, size_t lds, const rt_kernel_args* d, 
         return -1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
+    per_cu = per_cu > 2 ? 2 : per_cu;   // rt_resident_waves(): the per-wave buffers are sized for it
+    if ((long long)cus * per_cu * (block / 64) > (long long)rt_resident_waves()) return -1;
+    if (a.wbuf && (long long)cus * per_cu * (block / 64) > (long long)a.wbuf_waves) return -1;
     hipLaunchKernelGGL(kernel, dim3(cus * per_cu), dim3(block), lds, st, d);
     return 0;
 }
@@ -1519,16 +1643,18 @@ int rt_resident_waves(void) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    return cus * 2 * (512 / 64);   // default shape: 2 workgroups of 512 per CU
+    return cus * 2 * (512 / 64);   // every shape: at most 2 workgroups of 512 per CU (launch_persistent)
 }
 
 int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     // Variants (RT_KERNEL_VARIANT; all bit-identical, tests/test_gpu_boundary.py):
-    //   0 = 37: link-format nodes in LDS (+ the Perlin table and media records), 512 threads,
-    //           4 waves per SIMD; 38 its stats twin.  Falls back to 30 when the link format is
-    //           unavailable (> 2047 nodes) or does not fit LDS.
+    //   0: pooled units (render_pool) over link-format nodes in LDS (+ the Perlin table and
+    //      media records), 512 threads, 4 waves per SIMD; 39 its stats twin.  Falls back to the
+    //      threaded meta-word nodes (LDS, else global) when the link format is unavailable
+    //      (> 2047 nodes) or does not fit LDS.
+    //   37: the same walk with one pixel per lane (render_pixel); 38 its stats twin.
     //   30: threaded nodes with the meta word (in LDS when they fit, else global); 31 stats twin.
     //   61: the exact near-first stack walk (tree and stacks in LDS); 69 stats twin.
     // Every shape's dynamic LDS ends with the lanes' running-mean slots (RT_LDS_ACC_BYTES).
@@ -1541,7 +1667,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
                             : 0;
     const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
     const size_t lds_p = lds_t > extra_end ? lds_t : extra_end;
-    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69;
+    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39;
+    const bool pool = a.variant == 0 || a.variant == 39;
+    if (pool && !a.samples && !a.wbuf) return -1;   // pooled ordered / one-chunk units need the per-wave slots
     const size_t acc = RT_LDS_ACC_BYTES;
     // the launch shape and its staged bytes (before the running-mean slots)
     enum { FAST_LDS, FAST_GLOBAL, LINK_LDS, META_LDS, META_GLOBAL } shape;
@@ -1577,32 +1705,31 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     // the work-unit counter, then (ordered chunks) the tiles' published chunk counts
     const int n_tiles = ((a.width + 7) / 8) * ((a.local_rows + 7) / 8);
     if (hipMemsetAsync(a.tile_counter, 0, sizeof(int), st) != hipSuccess) return -1;
-    if (a.n_chunks > 1 && hipMemsetAsync(a.tile_done, 0, sizeof(unsigned) * (size_t)n_tiles, st) != hipSuccess)
+    if (a.n_chunks > 1 && !a.samples &&
+        hipMemsetAsync(a.tile_done, 0, sizeof(unsigned) * (size_t)n_tiles, st) != hipSuccess)
         return -1;
+    // the instantiations: <LINK, MINW, STATS, LDSN, BLOCK, FAST, OPT>
+#define RT_LAUNCH(LINK, LDSN, FAST, OPT)                                                                        \
+    (stats ? launch_persistent(render_persistent<LINK, 4, true, LDSN, 512, FAST, OPT>, 512, lds, a, d, st)    \
+           : launch_persistent(render_persistent<LINK, 4, false, LDSN, 512, FAST, OPT>, 512, lds, a, d, st))
     int rc;
     switch (shape) {
-        case FAST_LDS:
-            rc = stats ? launch_persistent(render_persistent<false, 4, true, true, 512, true>, 512, lds, d, st)
-                       : launch_persistent(render_persistent<false, 4, false, true, 512, true>, 512, lds, d, st);
-            break;
-        case FAST_GLOBAL:
-            rc = stats ? launch_persistent(render_persistent<false, 4, true, false, 512, true>, 512, lds, d, st)
-                       : launch_persistent(render_persistent<false, 4, false, false, 512, true>, 512, lds, d, st);
-            break;
-        case LINK_LDS:
-            rc = stats ? launch_persistent(render_persistent<true, 4, true, true, 512, false>, 512, lds, d, st)
-                       : launch_persistent(render_persistent<true, 4, false, true, 512, false>, 512, lds, d, st);
-            break;
+        case FAST_LDS: rc = RT_LAUNCH(false, true, true, 0); break;
+        case FAST_GLOBAL: rc = RT_LAUNCH(false, false, true, 0); break;
+        case LINK_LDS: rc = pool ? RT_LAUNCH(true, true, false, RT_OPT_POOL) : RT_LAUNCH(true, true, false, 0); break;
         case META_LDS:
-            rc = stats ? launch_persistent(render_persistent<false, 4, true, true, 512, false>, 512, lds, d, st)
-                       : launch_persistent(render_persistent<false, 4, false, true, 512, false>, 512, lds, d, st);
+            rc = pool ? RT_LAUNCH(false, true, false, RT_OPT_POOL) : RT_LAUNCH(false, true, false, 0);
             break;
         default:
-            rc = stats ? launch_persistent(render_persistent<false, 4, true, false, 512, false>, 512, lds, d, st)
-                       : launch_persistent(render_persistent<false, 4, false, false, 512, false>, 512, lds, d, st);
+            rc = pool ? RT_LAUNCH(false, false, false, RT_OPT_POOL) : RT_LAUNCH(false, false, false, 0);
             break;
     }
+#undef RT_LAUNCH
     if (rc) return rc;
+    if (a.samples) {   // staged chunks: the running mean over the launch's frames
+        const unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);
+        hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), 0, st, d);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
