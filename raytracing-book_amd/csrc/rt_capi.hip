@@ -113,6 +113,8 @@ struct rt_ctx {
     // applies the running mean in frame order.
     int chunk_target = 32;
     int stage_tiles = 4;
+    int sm_batch = 64;   // render_sm's shading batch (env RT_SM_BATCH) ...
+    int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
     size_t sample_budget = (size_t)16 << 30;
 };
 
@@ -709,12 +711,15 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) {
         // 0 = 37 (default), 30, 61 and their stats twins 38, 31, 69; anything else is the default
         const int want = std::atoi(v);
-        c->variant = (want == 30 || want == 31 || want == 37 || want == 38 || want == 39 || want == 61 || want == 69)
+        c->variant = (want == 30 || want == 31 || want == 37 || want == 38 || want == 39 || want == 40 || want == 41 ||
+                      want == 61 || want == 69)
                          ? want
                          : 0;
     }
     if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("RT_STAGE_TILES")) c->stage_tiles = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("RT_SM_BATCH")) c->sm_batch = std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_SM_FRAC")) c->sm_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
@@ -978,6 +983,8 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.uv_always = c->uv_always;
     a.boxes_canon = c->boxes_canon ? 1 : 0;
     a.variant = c->variant;
+    a.sm_batch = c->sm_batch;
+    a.sm_frac = c->sm_frac;
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);
@@ -1120,7 +1127,8 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             else if (staged) a.samples = (float4*)d.samples.ptr;
             a.wbuf = nullptr;
             a.wbuf_waves = 0;
-            if (!a.samples && (c->variant == 0 || c->variant == 39)) {   // pooled units fold per wave
+            if (!a.samples && (c->variant == 0 || c->variant == 39 || c->variant == 40 || c->variant == 41)) {
+                // pooled units fold per wave
                 const size_t need = (size_t)waves * 64 * (size_t)a.chunk_frames * sizeof(float4);
                 if (d.wbuf.bytes < need) {
                     dev_free(d.wbuf);
@@ -1336,6 +1344,7 @@ static int stats_twin(int v) {
     if (v == 61 || v == 69) return 69;
     if (v == 30 || v == 31) return 31;
     if (v == 37 || v == 38) return 38;
+    if (v == 40 || v == 41) return 41;
     return 39;
 }
 

@@ -98,6 +98,8 @@ struct rt_kernel_args {
     unsigned* fault;             // set when an ordered-chunk wait times out (rt_sync reports it)
     float4* wbuf;                // pooled units, ordered / one chunk: per resident wave 64 * chunk_frames colours
     int wbuf_waves;              // waves wbuf has slots for (the launch's grid never exceeds it)
+    int sm_batch;                // render_sm: shade once this many lanes' walks ended,
+    int sm_frac;                 // or this many 64ths of the lanes with a walk (or none runs)
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)

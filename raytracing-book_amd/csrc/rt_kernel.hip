@@ -37,7 +37,8 @@ namespace {
 typedef rt_kernel_args KP;
 
 // OPT bits of the kernel templates
-#define RT_OPT_POOL 1   // pooled units (render_pool): the default; without it a lane owns a pixel (variant 37)
+#define RT_OPT_POOL 1   // pooled units (render_pool): without it a lane owns a pixel (variant 37)
+#define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_sm)
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -58,7 +59,10 @@ enum {
     ST_FAST_PRE_CYC, ST_FAST_POST_CYC, ST_FAST_EXACT_CYC,
     // leaf stage by prim type: wave-cycles from the slot's start to the end of that type's test
     // (the types run one after another in this order, so each includes the ones before it)
-    ST_SPH_CYC, ST_QUAD_CYC, ST_BOX_CYC, ST_MED_CYC, ST_N
+    ST_SPH_CYC, ST_QUAD_CYC, ST_BOX_CYC, ST_MED_CYC,
+    // link walk: traces begun (wave calls, lanes), and rounds of its node-walk + leaf loop with the
+    // lanes whose trace is still running (the rest wait for the wave's longest trace)
+    ST_TRACE_IT, ST_TRACE_LN, ST_ROUND_IT, ST_ROUND_LN, ST_N
 };
 __device__ __forceinline__ bool first_active_lane() {
     unsigned long long m = __ballot(1);
@@ -508,7 +512,9 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
         const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
         const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
         uint32_t nx = 0u;
+        if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);
         for (;;) {
+            if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
             unsigned long long t0 = STATS ? clock64() : 0;
             nx = wave_exact ? link_walk<true, STATS>(base, nx, o, inv, tmin, tmax, st)
                             : link_walk<false, STATS>(base, nx, o, inv, tmin, tmax, st);
@@ -1204,6 +1210,25 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     return false;
 }
 
+// The rest of ray_color's loop body after the walk (compute.glsl:308-340): the
+// uv the walk left (compute.glsl:62), the background on a miss, else shade().
+__device__ __forceinline__ bool after_trace(const KP& P, Path& S, const Hit& h, bool hit, float px, float py,
+                                            v3& result) {
+    if (h.uv_kind_idx != 0) {
+        bool sph = (h.uv_kind_idx >> 16) == 1;
+        v3 up = add3(S.o, scale3(S.d, h.uv_a));   // the sphere hit's p (hitting.glsl:39)
+        S.uvs.kind_idx = h.uv_kind_idx;
+        S.uvs.a = sph ? up.x : h.uv_a;
+        S.uvs.b = sph ? up.y : h.uv_b;
+        S.uvs.c = sph ? up.z : S.uvs.c;
+    }
+    if (!hit) {
+        result = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
+        return true;
+    }
+    return shade(P, S, h, px, py, result);
+}
+
 // One iteration of ray_color's loop (compute.glsl:304-340).
 template <bool LINK, bool STATS, bool FAST, int OPT>
 __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc, Path& S,
@@ -1239,22 +1264,7 @@ __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ n
     }
     unsigned long long ts = STATS ? clock64() : 0;
     if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
-    // hit_record.uv as left by this walk (compute.glsl:62)
-    if (h.uv_kind_idx != 0) {
-        bool sph = (h.uv_kind_idx >> 16) == 1;
-        v3 up = add3(S.o, scale3(d, h.uv_a));   // the sphere hit's p (hitting.glsl:39)
-        S.uvs.kind_idx = h.uv_kind_idx;
-        S.uvs.a = sph ? up.x : h.uv_a;
-        S.uvs.b = sph ? up.y : h.uv_b;
-        S.uvs.c = sph ? up.z : S.uvs.c;
-    }
-    bool done;
-    if (!hit) {
-        result = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
-        done = true;
-    } else {
-        done = shade(P, S, h, px, py, result);
-    }
+    const bool done = after_trace(P, S, h, hit, px, py, result);
     if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
     return done;
 }
@@ -1353,6 +1363,20 @@ __device__ __forceinline__ void render_pixel(const KP& P, const float4* __restri
 // go to `out` by (frame-in-chunk, pixel slot = py * 8 + px): the unit's per-wave
 // slot (ordered / one chunk; the caller folds them in frame order) or, for
 // staged chunks, straight to P.samples.
+// Sample s of a pooled unit (frame-in-chunk * nv + pixel) to the wave's slot (by
+// frame-in-chunk and the pixel's slot py * 8 + px) or, staged, to P.samples.
+__device__ __forceinline__ void store_sample(const KP& P, float4* wslot, uint32_t s, uint32_t nv, int wt, int tx0,
+                                             int ly0, int f0, v3 cur) {
+    const uint32_t fl = s / nv, p = s - fl * nv;
+    const uint32_t py = p / (uint32_t)wt, px = p - py * (uint32_t)wt;
+    const float4 c4 = make_float4(cur.x, cur.y, cur.z, 0.0f);
+    if (wslot)
+        wslot[fl * 64u + py * 8u + px] = c4;
+    else
+        P.samples[(size_t)(f0 + (int)fl) * P.n_pixels + (uint32_t)(ly0 + (int)py) * (uint32_t)P.width +
+                  (uint32_t)(tx0 + (int)px)] = c4;
+}
+
 template <bool LINK, bool STATS, bool FAST, int OPT>
 __device__ __forceinline__ void render_pool(const KP& P, const float4* __restrict__ nodes, const FastCtx& fc,
                                             int tx0, int ly0, int wt, int ht, int f0, int kf, float4* wslot,
@@ -1388,15 +1412,136 @@ __device__ __forceinline__ void render_pool(const KP& P, const float4* __restric
         }
         v3 cur;
         if (bounce<LINK, STATS, FAST, OPT>(P, nodes, fc, S, fx, fy, cur, st)) {
-            const uint32_t fl = s / nv, p = s - fl * nv;
-            const uint32_t py = p / (uint32_t)wt, px = p - py * (uint32_t)wt;
-            const float4 c4 = make_float4(cur.x, cur.y, cur.z, 0.0f);
-            if (wslot)
-                wslot[fl * 64u + py * 8u + px] = c4;
-            else
-                P.samples[(size_t)(f0 + (int)fl) * P.n_pixels + (uint32_t)(ly0 + (int)py) * (uint32_t)P.width +
-                          (uint32_t)(tx0 + (int)px)] = c4;
+            store_sample(P, wslot, s, nv, wt, tx0, ly0, f0, cur);
             fresh = true;
+        }
+    }
+}
+
+// Pooled unit with the bounce split into stages (RT_OPT_SM, link-format walk):
+// every lane is FRESH (needs a sample), TRACE (its walk is running), HIT (walk
+// done, to be shaded) or RETIRED (no samples left).  The wave runs rounds of
+// node walk + leaf tests for its TRACE lanes until P.sm_batch lanes are HIT, or
+// P.sm_frac/64 of the lanes with a walk, or none is tracing, then shades the HIT lanes together; lanes whose path goes
+// on start their next walk, the others store their sample and claim the next.
+// So a lane whose walk ended early does not wait for the wave's longest walk:
+// it is shaded with the next batch while the other lanes' walks continue from
+// where they stopped (the walk position nx, ray_t.max and the hit record are
+// the lane's own, so each walk is the reference's, as in trace()).
+#define RT_SM_FRESH 0
+#define RT_SM_TRACE 1
+#define RT_SM_HIT 2
+#define RT_SM_RETIRED 3
+#define RT_SM_BEGIN 4   // a new walk: set up in the next pass
+template <bool STATS, int OPT>
+__device__ __forceinline__ void render_sm(const KP& P, const float4* __restrict__ nodes, int tx0, int ly0, int wt,
+                                          int ht, int f0, int kf, float4* wslot, unsigned long long* st) {
+    const uint32_t nv = (uint32_t)(wt * ht), total = nv * (uint32_t)kf;
+    const rt_camera_ubo& C = P.cam;
+    const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
+    const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
+    const int batch = P.sm_batch;
+    uint32_t next = 0;   // first unclaimed sample (the same in every lane)
+    uint32_t s = 0;
+    float fx = 0.0f, fy = 0.0f;
+    Path S;
+    Hit h;
+    bool has = false;
+    float tmax = RT_INFINITY, a = 0.0f;
+    v3 inv = mk3s(0.0f);
+    uint32_t nx = RT_LINK_END;
+    int status = RT_SM_FRESH;
+    for (;;) {
+        // claim samples for the FRESH lanes and start their paths (compute.glsl:345-350)
+        for (;;) {
+            const unsigned long long need = __ballot(status == RT_SM_FRESH);
+            if (need == 0) break;
+            if (status == RT_SM_FRESH) {
+                s = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                if (s >= total) {
+                    status = RT_SM_RETIRED;
+                } else {
+                    const uint32_t fl = s / nv, p = s - fl * nv;
+                    const int lr = ly0 + (int)(p / (uint32_t)wt), x = tx0 + (int)(p % (uint32_t)wt);
+                    const int y = ((lr / P.stripe_rows) * P.world + P.rank) * P.stripe_rows + lr % P.stripe_rows;
+                    fx = (float)x;
+                    fy = (float)y;
+                    unsigned long long t0 = STATS ? clock64() : 0;
+                    if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
+                    const v3 pbase = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)),
+                                          scale3(ld3(C.pixel_delta_v), fy));
+                    const int f = f0 + (int)fl;
+                    start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, pbase);
+                    if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
+                    if (P.max_depth <= 0) store_sample(P, wslot, s, nv, wt, tx0, ly0, f0, mk3s(0.0f));
+                    else status = RT_SM_BEGIN;   // a new walk
+                }
+            }
+            next += (uint32_t)__popcll(need);
+        }
+        // a new walk (bounce(): depth, a zero direction hits nothing, compute.glsl:226-229)
+        if (status == RT_SM_BEGIN) {
+            S.depth++;
+            h.t = 0.0f; h.type = 0; h.idx = 0; h.face = 0;
+            h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
+            has = false;
+            tmax = RT_INFINITY;
+            nx = 0u;
+            const bool dir_zero = (S.d.x == 0.0f) && (S.d.y == 0.0f) && (S.d.z == 0.0f);
+            status = (dir_zero || P.n_nodes == 0) ? RT_SM_HIT : RT_SM_TRACE;
+            if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);
+        }
+        // per-ray constants of every walk (new or resumed: the same values again)
+        if (status == RT_SM_TRACE) {
+            inv = mk3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
+            a = g_dot(S.d, S.d);
+        }
+        if (__ballot(status == RT_SM_TRACE || status == RT_SM_HIT) == 0) break;   // every lane retired
+        // rounds of node walk + leaf tests (trace())
+        for (;;) {
+            const unsigned long long tr = __ballot(status == RT_SM_TRACE);
+            const int n_hit = __popcll(__ballot(status == RT_SM_HIT));
+            if (tr == 0 || n_hit >= batch || n_hit * 64 >= P.sm_frac * (n_hit + __popcll(tr))) break;
+            const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
+            const bool wave_exact = __ballot(status == RT_SM_TRACE && lane_exact) != 0;
+            if (status == RT_SM_TRACE) {
+                if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
+                unsigned long long t0 = STATS ? clock64() : 0;
+                nx = wave_exact ? link_walk<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, st)
+                                : link_walk<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, st);
+                if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
+                if (nx == RT_LINK_END) {
+                    status = RT_SM_HIT;
+                } else {
+                    unsigned long long t1 = STATS ? clock64() : 0;
+                    if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+                    const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
+                    leaf_prims<STATS>(P, lf.x, lf.y, S.o, S.d, a, S.time, 0.001f, tmax, S.rf, fx, fy, h, has, st);
+                    if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+                    nx &= 0xFFFFu;
+                    if (nx == 0xFFFFu) status = RT_SM_HIT;
+                }
+            }
+        }
+        // shade the HIT lanes together
+        if (status == RT_SM_HIT) {
+            unsigned long long ts = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
+            v3 cur;
+            h.t = tmax;   // the accepted hit's t (unused on a miss)
+            bool done = after_trace(P, S, h, has, fx, fy, cur);
+            if (!done && S.depth >= P.max_depth) {   // the loop is exhausted: final_color stays vec3(0)
+                cur = mk3s(0.0f);
+                done = true;
+            }
+            if (done) {
+                store_sample(P, wslot, s, nv, wt, tx0, ly0, f0, cur);
+                status = RT_SM_FRESH;
+            } else {
+                status = RT_SM_BEGIN;
+            }
+            if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
         }
     }
 }
@@ -1534,8 +1679,12 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             const int tx0 = x - (lane & 7), ly0 = lr - (lane >> 3);
             float4* wslot =
                 ordered ? P.wbuf + ((size_t)blockIdx.x * (BLOCK / 64) + (tid >> 6)) * 64 * P.chunk_frames : nullptr;
-            render_pool<LINK, STATS, FAST, OPT>(P, rnodes, fc, tx0, ly0, min(8, P.width - tx0),
-                                                min(8, P.local_rows - ly0), f0, f1 - f0, wslot, st);
+            if (LINK && !FAST && (OPT & RT_OPT_SM))
+                render_sm<STATS, OPT>(P, rnodes, tx0, ly0, min(8, P.width - tx0), min(8, P.local_rows - ly0), f0,
+                                      f1 - f0, wslot, st);
+            else
+                render_pool<LINK, STATS, FAST, OPT>(P, rnodes, fc, tx0, ly0, min(8, P.width - tx0),
+                                                    min(8, P.local_rows - ly0), f0, f1 - f0, wslot, st);
             if (!ordered) continue;
             // the unit's colours, written by any lane of this wave, folded by the pixel's lane
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1650,11 +1799,12 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     // Variants (RT_KERNEL_VARIANT; all bit-identical, tests/test_gpu_boundary.py):
-    //   0: pooled units (render_pool) over link-format nodes in LDS (+ the Perlin table and
-    //      media records), 512 threads, 4 waves per SIMD; 39 its stats twin.  Falls back to the
-    //      threaded meta-word nodes (LDS, else global) when the link format is unavailable
-    //      (> 2047 nodes) or does not fit LDS.
-    //   37: the same walk with one pixel per lane (render_pixel); 38 its stats twin.
+    //   0: pooled units with walks and shading in batches (render_sm) over link-format nodes in
+    //      LDS (+ the Perlin table and media records), 512 threads, 4 waves per SIMD; 39 its stats
+    //      twin.  Falls back to pooled units over the threaded meta-word nodes (LDS, else global)
+    //      when the link format is unavailable (> 2047 nodes) or does not fit LDS.
+    //   40: pooled units, one bounce at a time for the whole wave (render_pool); 41 its stats twin.
+    //   37: the link walk with one pixel per lane (render_pixel); 38 its stats twin.
     //   30: threaded nodes with the meta word (in LDS when they fit, else global); 31 stats twin.
     //   61: the exact near-first stack walk (tree and stacks in LDS); 69 stats twin.
     // Every shape's dynamic LDS ends with the lanes' running-mean slots (RT_LDS_ACC_BYTES).
@@ -1667,8 +1817,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
                             : 0;
     const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
     const size_t lds_p = lds_t > extra_end ? lds_t : extra_end;
-    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39;
-    const bool pool = a.variant == 0 || a.variant == 39;
+    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39 || a.variant == 41;
+    const bool pool = a.variant == 0 || a.variant == 39 || a.variant == 40 || a.variant == 41;
+    const bool sm = a.variant == 0 || a.variant == 39;
     if (pool && !a.samples && !a.wbuf) return -1;   // pooled ordered / one-chunk units need the per-wave slots
     const size_t acc = RT_LDS_ACC_BYTES;
     // the launch shape and its staged bytes (before the running-mean slots)
@@ -1716,7 +1867,11 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     switch (shape) {
         case FAST_LDS: rc = RT_LAUNCH(false, true, true, 0); break;
         case FAST_GLOBAL: rc = RT_LAUNCH(false, false, true, 0); break;
-        case LINK_LDS: rc = pool ? RT_LAUNCH(true, true, false, RT_OPT_POOL) : RT_LAUNCH(true, true, false, 0); break;
+        case LINK_LDS:
+            rc = sm     ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM)
+                 : pool ? RT_LAUNCH(true, true, false, RT_OPT_POOL)
+                        : RT_LAUNCH(true, true, false, 0);
+            break;
         case META_LDS:
             rc = pool ? RT_LAUNCH(false, true, false, RT_OPT_POOL) : RT_LAUNCH(false, true, false, 0);
             break;

@@ -14,7 +14,7 @@ NAMES = ["TOTAL", "START_CYC", "START_IT", "START_LN", "NODE_CYC", "NODE_IT", "N
          "LEAF_LN", "SPH_LN", "QUAD_LN", "BOX_LN", "MED_LN", "SHADE_CYC", "SHADE_IT", "SHADE_LN", "SPH_IT",
          "QUAD_IT", "BOX_IT", "MED_IT", "FAST_TRACES", "FAST_EXACT"] + [f"FAST_WHY{r}" for r in range(1, 10)] + [
          "FAST_STEPS", "FAST_TESTS", "FAST_PRE_CYC", "FAST_POST_CYC", "FAST_EXACT_CYC",
-         "SPH_CYC", "QUAD_CYC", "BOX_CYC", "MED_CYC"]
+         "SPH_CYC", "QUAD_CYC", "BOX_CYC", "MED_CYC", "TRACE_IT", "TRACE_LN", "ROUND_IT", "ROUND_LN"]
 
 
 def main():
@@ -50,6 +50,10 @@ def main():
         cyc = v[t + "_CYC"]
         print(f"  leaf-slot {t:4s}: wave-executions {it:.3e} lanes/exec {ln / max(it, 1):5.2f}  per-sample {ln / samples:5.2f}"
               f"  {100.0 * cyc / tot:5.1f}% of wave-cycles  cyc/exec {cyc / max(it, 1):7.1f}")
+    if v["TRACE_IT"]:
+        print(f"  link walk: {v['TRACE_LN'] / v['TRACE_IT']:5.2f} lanes per wave trace, "
+              f"{v['ROUND_IT'] / v['TRACE_IT']:5.2f} node-walk+leaf rounds per wave trace, "
+              f"{v['ROUND_LN'] / (64.0 * max(v['ROUND_IT'], 1)) * 100:5.1f}% of lanes still tracing per round")
     print("raw", v)
 
 

@@ -1,0 +1,5 @@
+export TMPDIR=/tmp; mkdir -p gpurun_out
+step() { local name=$1 to=$2; shift 2; echo "== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; grep -v "^raw" "gpurun_out/$name.log" | tail -14 ; [ $rc -eq 0 ] || exit $rc; }
+step kstats_pool 300 python tools/kernel_stats.py --scene 8 --frames 64
+
+exit 0

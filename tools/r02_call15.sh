@@ -1,0 +1,9 @@
+export TMPDIR=/tmp; mkdir -p gpurun_out
+step() { local name=$1 to=$2; shift 2; echo "== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; grep -v "^raw" "gpurun_out/$name.log" | grep "median\|DIFFER\|passed\|failed\|Error\|error\|link walk\|%" ; [ $rc -eq 0 ] || exit $rc; }
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+step ab_n1 400 python tools/ab_variants.py --variants 0,40,0b8,0b16,0b24,0b48,0b64 --frames 64 --rounds 5 --scene 8
+step ab_s0 400 python tools/ab_variants.py --variants 0,40,0b16 --frames 64 --rounds 5 --scene 0
+step ab_s6 400 python tools/ab_variants.py --variants 0,40,0b16 --frames 64 --rounds 5 --scene 6
+step ab_n8r0 400 python tools/ab_variants.py --variants 0,40 --rank 0 --world 8 --frames 256 --rounds 5 --scene 8
+step kstats_sm 300 python tools/kernel_stats.py --scene 8 --frames 64
+exit 0
