@@ -100,6 +100,8 @@ struct rt_ctx {
     int debug_flags = 0;    // env RT_DEBUG_FLAGS: ablation runs only (bit 0: Perlin -> 0.5)
     bool uv_always = false;
     bool boxes_canon = false;   // every box has Box.java's axis-aligned face layout (dboxes[18..20])
+    bool fd_ok[6] = {true, true, true, true, true, true};   // per binding: records in the fast-division regime
+    bool fd_cam = true;
     bool validated = false;
     uint64_t last_ns = 0;
     int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
@@ -113,6 +115,7 @@ struct rt_ctx {
     // applies the running mean in frame order.
     int chunk_target = 32;
     int stage_tiles = 4;
+    bool fastdiv = true;   // shared-reciprocal divisions where exact (env RT_FASTDIV=0 disables; A/B)
     int sm_batch = 64;   // render_sm's shading batch (env RT_SM_BATCH) ...
     int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
     size_t sample_budget = (size_t)16 << 30;
@@ -615,6 +618,17 @@ void face_record(const rt_quad& q, float4 out[3]) {
     out[2] = make_float4(v[a], v[b], delta, csf);
 }
 
+// The scene side of the shared-reciprocal division regime (rt_kernel.hip rcp_nr /
+// div_nr): coordinates within 2^20 (so are the rays' origins and directions: hit
+// points, camera rays, scatter and light-sampling directions), a face's delta
+// normal within [2^-60, 2^20].
+bool fd_coord(float x) { return std::fabs(x) <= 1048576.0f; }
+bool fd_face(const float4 f[3]) {
+    const float ad = std::fabs(f[2].z);
+    return fd_coord(f[0].w) && fd_coord(f[1].x) && fd_coord(f[1].y) && fd_coord(f[1].z) && fd_coord(f[1].w) &&
+           fd_coord(f[2].x) && fd_coord(f[2].y) && ad >= 0x1p-60f && ad <= 0x1p20f;
+}
+
 int validate(rt_ctx* c) {
     if (c->validated) return RT_OK;
     size_t ns = c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere);
@@ -718,6 +732,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     }
     if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("RT_STAGE_TILES")) c->stage_tiles = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("RT_FASTDIV")) c->fastdiv = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_SM_BATCH")) c->sm_batch = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SM_FRAC")) c->sm_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
@@ -799,8 +814,12 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
         const rt_quad* qs = (const rt_quad*)bytes;
         size_t nq = nbytes / sizeof(rt_quad);   // a box is 6 consecutive quads
         faces.resize(binding == RT_BIND_QUADS ? nq * RT_DFACE_F4 : (nq / 6) * RT_DBOX_F4);
+        bool fd = true;
         if (binding == RT_BIND_QUADS) {
-            for (size_t k = 0; k < nq; k++) face_record(qs[k], &faces[k * RT_DFACE_F4]);
+            for (size_t k = 0; k < nq; k++) {
+                face_record(qs[k], &faces[k * RT_DFACE_F4]);
+                fd = fd && fd_face(&faces[k * RT_DFACE_F4]);
+            }
         } else {
             // per box: the 6 planes first, then the 6 (A, B) pairs, then the canonical
             // planes (RT_DBOX_F4 float4)
@@ -811,6 +830,7 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
                 for (int i = 0; i < 6; i++) {
                     float4 f[3];
                     face_record(qs[bx * 6 + i], f);
+                    fd = fd && fd_face(f);
                     o[i] = f[0];
                     o[6 + 2 * i] = f[1];
                     o[7 + 2 * i] = f[2];
@@ -825,7 +845,21 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
                 o[18] = make_float4(sw[0], sw[1], sw[2], sw[3]);
                 o[19] = make_float4(sw[4], sw[5], sw[6], sw[7]);
                 o[20] = make_float4(sw[8], sw[9], sw[10], sw[11]);
-            }        }
+                // the canonical test shares one reciprocal per axis: opposite faces' normals negated
+                if (sw[4] != -sw[0] || sw[6] != -sw[2] || sw[10] != -sw[8]) fd = false;
+            }
+        }
+        c->fd_ok[binding] = fd;
+    }
+    if (binding == RT_BIND_SPHERES) {
+        const rt_sphere* sp = (const rt_sphere*)bytes;
+        bool fd = true;
+        const float L = 524288.0f;   // center1 + center_vec * time within 2^20
+        for (size_t k = 0; k < nbytes / sizeof(rt_sphere); k++)
+            for (int i = 0; i < 3; i++)
+                fd = fd && std::fabs(sp[k].center1[i]) <= L && std::fabs(sp[k].center_vec[i]) <= L &&
+                     std::fabs(sp[k].radius) <= L;
+        c->fd_ok[binding] = fd;
     }
     if (binding == RT_BIND_LIGHTS) {
         src = (const uint8_t*)bytes + 4;
@@ -884,6 +918,8 @@ int rt_set_camera(rt_ctx* c, const float ubo[28]) {
     if (!c || !ubo) return set_err(c, RT_ERR_INVALID_ARG, "NULL camera");
     std::memcpy(&c->cam, ubo, sizeof(rt_camera_ubo));
     c->have_cam = true;
+    c->fd_cam = true;   // the camera's points and vectors within the fast-division regime's 2^20
+    for (int i = 0; i < 28; i++) c->fd_cam = c->fd_cam && fd_coord(ubo[i]);
     return RT_OK;
 }
 
@@ -982,6 +1018,10 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.lights_count = lc;
     a.uv_always = c->uv_always;
     a.boxes_canon = c->boxes_canon ? 1 : 0;
+    a.fastdiv = (c->fastdiv && c->fd_cam && c->fd_ok[RT_BIND_SPHERES] && c->fd_ok[RT_BIND_QUADS] &&
+                 c->fd_ok[RT_BIND_BOXES])
+                    ? 1
+                    : 0;
     a.variant = c->variant;
     a.sm_batch = c->sm_batch;
     a.sm_frac = c->sm_frac;

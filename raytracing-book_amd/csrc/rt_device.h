@@ -103,6 +103,7 @@ struct rt_kernel_args {
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
+    int fastdiv;                 // the scene's records are in the shared-reciprocal division regime
     int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1
     int perlin_lds;              // its float4 offset in the dynamic LDS (after the nodes), or -1
     int n_media;

@@ -39,6 +39,7 @@ typedef rt_kernel_args KP;
 // OPT bits of the kernel templates
 #define RT_OPT_POOL 1   // pooled units (render_pool): without it a lane owns a pixel (variant 37)
 #define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_sm)
+#define RT_OPT_FD 4     // with RT_OPT_SM: the scene is in the shared-reciprocal division regime (P.fastdiv)
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -112,10 +113,40 @@ struct Hit {
     float uv_a, uv_b;   // sphere: t of that hit; quad: (alpha, beta)
 };
 
+// ------------------------------------------------------- shared-reciprocal division
+// The compiler's f32 division num / den is: v_div_scale of den and of num, v_rcp,
+// two refinement fmas (the reciprocal r), q0 = num * r, e2 = num - den * q0,
+// q1 = q0 + e2 * r, e3 = num - den * q1, v_div_fmas (q1 + e3 * r), v_div_fixup.
+// v_div_scale returns its operand unchanged (and v_div_fmas is that plain fma)
+// unless num or den is zero or denormal, 1/den or num/den would be denormal, or
+// the exponents are 96 or more apart; v_div_fixup returns q itself unless an
+// input is zero, inf or NaN or the quotient over/underflows.  Outside those
+// cases rcp_nr + div_nr below are the same operations, so the same bits, and r
+// depends on den alone: quotients with one denominator share it (3 + 5 VALU
+// instead of 11 each).  Callers use them only where every quotient they keep is
+// in that regime (below); tests/test_gpu_parity.py compares both forms bit for bit.
+__device__ __forceinline__ float rcp_nr(float den) {
+    const float r0 = __builtin_amdgcn_rcpf(den);
+    return fmaf(fmaf(-den, r0, 1.0f), r0, r0);
+}
+__device__ __forceinline__ float div_nr(float num, float den, float r) {
+    const float q0 = num * r;
+    const float q1 = fmaf(fmaf(-den, q0, num), r, q0);
+    return fmaf(fmaf(-den, q1, num), r, q1);
+}
+// Where the leaf tests use them (FD kernels, P.fastdiv: the camera and every record
+// within 2^20, faces' delta in [2^-60, 2^20]), every kept quotient is in that
+// regime: a box or quad plane divides by a denominator of at least 1e-8 (smaller
+// ones skip the face) and at most the scene's size, and a numerator so small that
+// the quotient would be below tmin = 0.001 is rejected either way; a sphere root
+// divides by dot(dir, dir), checked >= 2^-60 per wave (else '/'), which bounds the
+// exponent gap by ~52; alpha and beta fall back to '/' for a numerator below
+// 2^-100 (a tiny alpha >= 0 is kept).
 // ------------------------------------------------------------- primitives
-// hitting.glsl:17-38 — the root only.
+// hitting.glsl:17-38 — the root only.  fd: the roots as div_nr with ra =
+// rcp_nr(a), unless a lane's a = dot(dir, dir) is below 2^-60.
 __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
-                                         float tmax, float& t) {
+                                         float tmax, float& t, bool fd = false, float ra = 0.0f) {
     float4 A = sp[0], B = sp[1];
     v3 center = add3(f3(A), scale3(f3(B), time));
     v3 oc = sub3(o, center);
@@ -124,9 +155,10 @@ __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float ti
     float disc = half_b * half_b - a * c;
     if (disc < 0.0f) return false;
     float sq = sqrtf(disc);
-    float root = (-half_b - sq) / a;
+    fd = fd && __ballot(!(a >= 0x1p-60f)) == 0;
+    float root = fd ? div_nr(-half_b - sq, a, ra) : (-half_b - sq) / a;
     if (!(tmin < root && root < tmax)) {
-        root = (-half_b + sq) / a;
+        root = fd ? div_nr(-half_b + sq, a, ra) : (-half_b + sq) / a;
         if (!(tmin < root && root < tmax)) return false;
     }
     t = root;
@@ -139,27 +171,39 @@ __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float ti
 // computed delta with the reference's expression, so alpha/beta here are the
 // reference's values: intersection = o + dir*t, ph = intersection - q, then the
 // 2-D Cramer quotients on the chosen pair of axes.
-__device__ __forceinline__ bool face_interior(float4 A, float4 B, v3 o, v3 d, float t, float& alpha, float& beta) {
+// fd: alpha and beta share delta's reciprocal (delta within [2^-60, 2^20], host
+// check) unless a lane's numerator is below 2^-100 in magnitude (or zero), the
+// one case where a kept value (0 <= alpha <= 1) could leave the regime.
+__device__ __forceinline__ bool face_interior(float4 A, float4 B, v3 o, v3 d, float t, float& alpha, float& beta,
+                                              bool fd = false) {
     const int cs = __float_as_int(B.w);
     float oa = (cs == 2) ? o.y : o.x, da = (cs == 2) ? d.y : d.x;
     float ob = (cs == 0) ? o.y : o.z, db = (cs == 0) ? d.y : d.z;
     float pa = (oa + da * t) - A.x;
     float pb = (ob + db * t) - A.y;
-    alpha = (pa * B.y - pb * B.x) / B.z;
-    beta = (pb * A.z - pa * A.w) / B.z;
+    const float na = pa * B.y - pb * B.x, nb = pb * A.z - pa * A.w;
+    if (fd && __ballot(!(fabsf(na) >= 0x1p-100f && fabsf(nb) >= 0x1p-100f)) == 0) {
+        const float r = rcp_nr(B.z);
+        alpha = div_nr(na, B.z, r);
+        beta = div_nr(nb, B.z, r);
+    } else {
+        alpha = na / B.z;
+        beta = nb / B.z;
+    }
     return (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
 }
 
 // hitting.glsl:90-133 without the record writes; f = dquads record.
 __device__ __forceinline__ bool quad_test(const float4* __restrict__ f, v3 o, v3 d, float tmin, float tmax, float& t,
-                                          float& alpha, float& beta) {
+                                          float& alpha, float& beta, bool fd = false) {
     float4 Q0 = f[0];
     v3 n = f3(Q0);
     float denom = g_dot(n, d);
     if (fabsf(denom) < 1e-8f) return false;
-    float tt = (Q0.w - g_dot(n, o)) / denom;
+    const float num = Q0.w - g_dot(n, o);
+    float tt = fd ? div_nr(num, denom, rcp_nr(denom)) : num / denom;
     if (!(tmin <= tt && tt <= tmax)) return false;
-    if (!face_interior(f[1], f[2], o, d, tt, alpha, beta)) return false;
+    if (!face_interior(f[1], f[2], o, d, tt, alpha, beta, fd)) return false;
     t = tt;
     return true;
 }
@@ -170,7 +214,7 @@ __device__ __forceinline__ bool quad_test(const float4* __restrict__ f, v3 o, v3
 // reference's sequential test tmin <= t_i <= current max, and only those reach
 // the interior test — the same tests on the same values, so the same result.
 __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3 d, float tmin, float tmax, float& t,
-                                         int& face, float& alpha, float& beta) {
+                                         int& face, float& alpha, float& beta, bool fd = false) {
     bool has = false;
     // two halves of three faces: fewer live registers than six at once
 #pragma unroll
@@ -190,7 +234,7 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
             const int i = h + k;
             if ((cand >> k) & 1u) {
                 float al, be;
-                if (ti[k] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[k], al, be)) {
+                if (ti[k] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[k], al, be, fd)) {
                     tmax = ti[k];
                     t = ti[k];
                     face = i;
@@ -209,9 +253,13 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
 // dot(n, d) = s_i*d_k and dot(n, o) = s_i*o_k exactly (the other products are
 // exact zeros; a zero sign differs only where the face is skipped or t is 0 <
 // tmin).  The planes come from the record's compact tail (fb[18..20]).
+// fd (P.fastdiv also guarantees s_2 = -s_0, s_3 = -s_1, s_5 = -s_4): each axis'
+// pair of faces divides by +-(s * d_k), so one reciprocal per axis, negated for the
+// opposite face; a plane t is kept only when >= tmin = 0.001, never in the
+// tiny-numerator case.
 __device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, const float4* __restrict__ fb, v3 o,
                                                v3 d, float tmin, float tmax, float& t, int& face, float& alpha,
-                                               float& beta) {
+                                               float& beta, bool fd = false) {
     const float4 c0 = pl[0], c1 = pl[1], c2 = pl[2];
     const float sv[6] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z};
     const float wv[6] = {c0.y, c0.w, c1.y, c1.w, c2.y, c2.w};
@@ -219,18 +267,32 @@ __device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, co
     const float ok[6] = {o.z, o.x, o.z, o.x, o.y, o.y};
     float ti[6];
     unsigned cand = 0;
+    if (fd) {
+        // by axis: faces (0, 2), (1, 3), (4, 5)
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-        const float denom = sv[i] * dk[i];
-        ti[i] = (wv[i] - sv[i] * ok[i]) / denom;   // unused when |denom| < 1e-8
-        if (!(fabsf(denom) < 1e-8f) && (tmin <= ti[i] && ti[i] <= tmax)) cand |= 1u << i;
+        for (int k = 0; k < 3; k++) {
+            const int i = k == 2 ? 4 : k, j = k == 2 ? 5 : k + 2;
+            const float den_i = sv[i] * dk[i], den_j = sv[j] * dk[j];
+            const float r = rcp_nr(den_i);
+            ti[i] = div_nr(wv[i] - sv[i] * ok[i], den_i, r);   // unused when |denom| < 1e-8
+            ti[j] = div_nr(wv[j] - sv[j] * ok[j], den_j, -r);
+            if (!(fabsf(den_i) < 1e-8f) && (tmin <= ti[i] && ti[i] <= tmax)) cand |= 1u << i;
+            if (!(fabsf(den_j) < 1e-8f) && (tmin <= ti[j] && ti[j] <= tmax)) cand |= 1u << j;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const float denom = sv[i] * dk[i];
+            ti[i] = (wv[i] - sv[i] * ok[i]) / denom;   // unused when |denom| < 1e-8
+            if (!(fabsf(denom) < 1e-8f) && (tmin <= ti[i] && ti[i] <= tmax)) cand |= 1u << i;
+        }
     }
     bool has = false;
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         if ((cand >> i) & 1u) {
             float al, be;
-            if (ti[i] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[i], al, be)) {
+            if (ti[i] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[i], al, be, fd)) {
                 tmax = ti[i];
                 t = ti[i];
                 face = i;
@@ -399,10 +461,12 @@ __device__ __forceinline__ bool aabb_pk(float4 n0, float4 n1, v3 o, v3 inv, floa
 }
 
 // The two prims of a leaf (compute.glsl:247-256), left then right.
-template <bool STATS>
-__device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a, float time,
-                                           float tmin, float& tmax, float& rf, float px, float py, Hit& h, bool& has,
-                                           unsigned long long* st) {
+// FD: the shared-reciprocal divisions (rcp_nr / div_nr; FD kernels only).
+template <bool STATS, bool FD>
+__device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a,
+                                             float time, float tmin, float& tmax, float& rf, float px, float py, Hit& h,
+                                             bool& has, unsigned long long* st) {
+    constexpr bool fd = FD;
     // finite origin and direction: the canonical box planes equal the reference's dot products
     const bool fin = fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY &&
                      fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY;
@@ -421,17 +485,18 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
         bool hit = false;
         unsigned long long c0 = STATS ? clock64() : 0;
         if (ty == RT_MODEL_SPHERE) {
-            hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t);
+            hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t, fd,
+                           fd ? rcp_nr(a) : 0.0f);
             if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
             if (STATS) st_add(st, ST_SPH_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_QUAD) {
-            hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, tmax, t, al, be);
+            hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, tmax, t, al, be, fd);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_QUAD_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_BOX) {
             hit = (P.boxes_canon && fin) ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix + 18, P.dboxes + RT_DBOX_F4 * ix, o,
-                                                          d, tmin, tmax, t, face, al, be)
-                                         : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be);
+                                                          d, tmin, tmax, t, face, al, be, fd)
+                                         : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be, fd);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
@@ -445,6 +510,7 @@ __device__ __forceinline__ void leaf_prims(const KP& P, uint32_t meta, uint32_t 
         }
     }
 }
+
 
 // The link-format node loop from byte offset nx until a hit leaf or the end of
 // the walk (sign bit).  EXACT: the reference's per-axis slab (a -inf in 1/dir);
@@ -523,7 +589,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
             unsigned long long t1 = STATS ? clock64() : 0;
             if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
             const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
-            leaf_prims<STATS>(P, lf.x, lf.y, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            leaf_prims_t<STATS, false>(P, lf.x, lf.y, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
             if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
             nx &= 0xFFFFu;
             if (nx == 0xFFFFu) break;
@@ -563,7 +629,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
         if (!leaf) break;
         unsigned long long t1 = STATS ? clock64() : 0;
         if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-        leaf_prims<STATS>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+        leaf_prims_t<STATS, false>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
         if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
     }
     return has;
@@ -1433,7 +1499,9 @@ __device__ __forceinline__ void render_pool(const KP& P, const float4* __restric
 #define RT_SM_HIT 2
 #define RT_SM_RETIRED 3
 #define RT_SM_BEGIN 4   // a new walk: set up in the next pass
-template <bool STATS, int OPT>
+// FD (P.fastdiv): the rounds' leaf tests use the shared-reciprocal divisions (one
+// form of the leaf code per kernel keeps the hot loop's registers).
+template <bool STATS, int OPT, bool FD>
 __device__ __forceinline__ void render_sm(const KP& P, const float4* __restrict__ nodes, int tx0, int ly0, int wt,
                                           int ht, int f0, int kf, float4* wslot, unsigned long long* st) {
     const uint32_t nv = (uint32_t)(wt * ht), total = nv * (uint32_t)kf;
@@ -1517,7 +1585,8 @@ __device__ __forceinline__ void render_sm(const KP& P, const float4* __restrict_
                     unsigned long long t1 = STATS ? clock64() : 0;
                     if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
                     const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
-                    leaf_prims<STATS>(P, lf.x, lf.y, S.o, S.d, a, S.time, 0.001f, tmax, S.rf, fx, fy, h, has, st);
+                    leaf_prims_t<STATS, FD>(P, lf.x, lf.y, S.o, S.d, a, S.time, 0.001f, tmax, S.rf, fx, fy, h, has,
+                                            st);
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
                     nx &= 0xFFFFu;
                     if (nx == 0xFFFFu) status = RT_SM_HIT;
@@ -1680,8 +1749,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             float4* wslot =
                 ordered ? P.wbuf + ((size_t)blockIdx.x * (BLOCK / 64) + (tid >> 6)) * 64 * P.chunk_frames : nullptr;
             if (LINK && !FAST && (OPT & RT_OPT_SM))
-                render_sm<STATS, OPT>(P, rnodes, tx0, ly0, min(8, P.width - tx0), min(8, P.local_rows - ly0), f0,
-                                      f1 - f0, wslot, st);
+                render_sm<STATS, OPT, (OPT & RT_OPT_FD) != 0>(P, rnodes, tx0, ly0, min(8, P.width - tx0),
+                                                              min(8, P.local_rows - ly0), f0, f1 - f0, wslot, st);
             else
                 render_pool<LINK, STATS, FAST, OPT>(P, rnodes, fc, tx0, ly0, min(8, P.width - tx0),
                                                     min(8, P.local_rows - ly0), f0, f1 - f0, wslot, st);
@@ -1762,6 +1831,10 @@ __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const f
         case 4: r = g_atan2(x[i], y ? y[i] : 1.0f); break;
         case 5: r = g_fract(x[i]); break;
         case 6: r = sqrtf(x[i]); break;
+        // the leaf tests' division forms (rcp_nr / div_nr) against the compiler's '/'
+        case 100: r = x[i] / y[i]; break;
+        case 101: r = div_nr(x[i], y[i], rcp_nr(y[i])); break;
+        case 102: r = div_nr(x[i], y[i], -rcp_nr(-y[i])); break;   // an opposite face's shared reciprocal
         default: break;
     }
     out[i] = r;
@@ -1868,7 +1941,8 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
         case FAST_LDS: rc = RT_LAUNCH(false, true, true, 0); break;
         case FAST_GLOBAL: rc = RT_LAUNCH(false, false, true, 0); break;
         case LINK_LDS:
-            rc = sm     ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM)
+            rc = sm && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD)
+                 : sm   ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM)
                  : pool ? RT_LAUNCH(true, true, false, RT_OPT_POOL)
                         : RT_LAUNCH(true, true, false, 0);
             break;

@@ -69,3 +69,39 @@ def test_builtins_bit_exact_on_device(gpu):
                                      out.ctypes.data_as(fp), x.size)
         assert rc == 0
         assert bit_equal(out, ref), f"{name}: {mismatch_report(out[:, None], ref[:, None])}"
+
+
+def test_shared_reciprocal_division_bit_exact(gpu):
+    """rcp_nr / div_nr (rt_kernel.hip), the leaf tests' division by a shared
+    reciprocal, give the bits of the compiler's '/' -- and of IEEE division
+    (numpy) -- for every quotient in the regime the kernel uses them in: operands
+    and quotient normal, numerator above 2^-103, exponents less than 96 apart.
+    Also with the reciprocal of the negated denominator, negated (box faces)."""
+    import ctypes
+    rng = np.random.default_rng(7)
+    L = rtamd.amd()
+    n = 1 << 22
+    num = (rng.choice([-1.0, 1.0], n) * np.exp2(rng.uniform(-100, 60, n)) * rng.uniform(1, 2, n)).astype(np.float32)
+    den = (rng.choice([-1.0, 1.0], n) * np.exp2(rng.uniform(-62, 62, n)) * rng.uniform(1, 2, n)).astype(np.float32)
+    # mantissas next to powers of two, where the reciprocal is least accurate
+    k = n // 8
+    den[:k] = (np.exp2(rng.integers(-30, 30, k)) * (1 + rng.integers(-64, 64, k) * 2.0 ** -23)).astype(np.float32)
+    num[k:2 * k] = (np.exp2(rng.integers(-30, 30, k)) * (2 - rng.integers(1, 64, k) * 2.0 ** -23)).astype(np.float32)
+    q64 = num.astype(np.float64) / den.astype(np.float64)
+    en, ed = np.frexp(num)[1], np.frexp(den)[1]
+    regime = ((np.abs(num) >= 2.0 ** -103) & (np.abs(den) >= 2.0 ** -125) & (np.abs(den) <= 2.0 ** 125) &
+              (en - ed < 96) & (np.abs(q64) >= 2.0 ** -125) & (np.abs(q64) < 2.0 ** 127))
+    assert regime.mean() > 0.8
+    num, den = num[regime], den[regime]
+    fp = ctypes.POINTER(ctypes.c_float)
+    outs = {}
+    for fn in (100, 101, 102):
+        out = np.empty_like(num)
+        assert L.rt_debug_eval_builtin(0, fn, num.ctypes.data_as(fp), den.ctypes.data_as(fp),
+                                       out.ctypes.data_as(fp), num.size) == 0
+        outs[fn] = out.view(np.uint32)
+    ieee = (num / den).view(np.uint32)
+    assert (outs[100] == ieee).all(), int((outs[100] != ieee).sum())
+    for fn in (101, 102):
+        bad = np.flatnonzero(outs[fn] != outs[100])
+        assert bad.size == 0, (fn, bad.size, num[bad[:4]], den[bad[:4]])
