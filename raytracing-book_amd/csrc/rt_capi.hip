@@ -118,6 +118,7 @@ struct rt_ctx {
     bool fastdiv = true;   // shared-reciprocal divisions where exact (env RT_FASTDIV=0 disables; A/B)
     int sm_batch = 64;   // render_sm's shading batch (env RT_SM_BATCH) ...
     int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
+    int walk_frac = 48;  // render_sm: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
     size_t sample_budget = (size_t)16 << 30;
 };
 
@@ -735,6 +736,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_FASTDIV")) c->fastdiv = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_SM_BATCH")) c->sm_batch = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SM_FRAC")) c->sm_frac = std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_WALK_FRAC")) c->walk_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
@@ -1025,6 +1027,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.variant = c->variant;
     a.sm_batch = c->sm_batch;
     a.sm_frac = c->sm_frac;
+    a.walk_frac = c->walk_frac;
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);

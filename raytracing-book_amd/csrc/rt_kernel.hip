@@ -553,6 +553,47 @@ __device__ __forceinline__ uint32_t link_walk(const char* __restrict__ base, uin
     return nx;
 }
 
+// link_walk for a wave's walking lanes that stops once `need` of them hold a hit
+// leaf or have ended (the others keep their position nx >= 0 and go on in the
+// next round): the wave does not step its last walkers alone while the lanes
+// waiting at a leaf idle.  Checked every second step.
+template <bool EXACT, bool STATS>
+__device__ __forceinline__ uint32_t link_walk_part(const char* __restrict__ base, uint32_t nx, v3 o, v3 inv,
+                                                   float tmin, float tmax, int need, unsigned long long* st) {
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if ((int)nx >= 0) {
+                if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
+                float4 n0, n1;
+                if (STATS) {
+                    n0 = *reinterpret_cast<const float4*>(base + nx);
+                    n1 = *reinterpret_cast<const float4*>(base + nx + 16);
+                } else {
+                    const lds_f4* p = (const lds_f4*)(uintptr_t)nx;
+                    const f4v a = p[0], b = p[1];
+                    n0 = make_float4(a.x, a.y, a.z, a.w);
+                    n1 = make_float4(b.x, b.y, b.z, b.w);
+                }
+                bool hit;
+                if (!EXACT) {
+                    hit = aabb_pk(n0, n1, o, inv, tmin, tmax);
+                } else {
+                    float lo = tmin, hi = tmax;
+                    slab(n0.x, n0.y, o.x, inv.x, lo, hi);
+                    slab(n0.z, n0.w, o.y, inv.y, lo, hi);
+                    slab(n1.x, n1.y, o.z, inv.z, lo, hi);
+                    hit = !(hi <= lo);
+                }
+                nx = __float_as_uint(hit ? n1.z : n1.w);
+            }
+        }
+        const unsigned long long walking = __ballot((int)nx >= 0);
+        if (walking == 0 || __popcll(__ballot(1) & ~walking) >= need) break;
+    }
+    return nx;
+}
+
 // compute.glsl:226-266 over the threaded BVH.  Each lane's node sequence is the
 // reference's; only the interleaving of a wave's lanes differs: lanes advance
 // through inner/missed nodes until each holds a hit leaf (or is done), then the
@@ -1576,10 +1617,18 @@ __device__ __forceinline__ void render_sm(const KP& P, const float4* __restrict_
             if (status == RT_SM_TRACE) {
                 if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
                 unsigned long long t0 = STATS ? clock64() : 0;
-                nx = wave_exact ? link_walk<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, st)
-                                : link_walk<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, st);
+                if (P.walk_frac >= 64) {
+                    nx = wave_exact ? link_walk<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, st)
+                                    : link_walk<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, st);
+                } else {
+                    const int need = (__popcll(__ballot(1)) * P.walk_frac + 63) >> 6;
+                    nx = wave_exact ? link_walk_part<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, need, st)
+                                    : link_walk_part<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, need, st);
+                }
                 if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
-                if (nx == RT_LINK_END) {
+                if ((int)nx >= 0) {
+                    // still walking: the next round goes on from nx
+                } else if (nx == RT_LINK_END) {
                     status = RT_SM_HIT;
                 } else {
                     unsigned long long t1 = STATS ? clock64() : 0;
