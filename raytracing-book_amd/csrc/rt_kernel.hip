@@ -47,6 +47,19 @@ extern __shared__ float4 rt_dyn_lds[];
 
 __device__ __forceinline__ v3 f3(float4 v) { return mk3(v.x, v.y, v.z); }
 
+// Scene records through global-address-space loads (global_load, not flat): the
+// record pointers come from the argument block, so the compiler cannot infer
+// their address space; flat loads also count against the LDS counter, which makes
+// the walk's LDS reads wait on them.
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const f4v g_f4v;
+typedef __attribute__((address_space(1))) const float g_f;
+typedef __attribute__((address_space(3))) const float lds_f;
+__device__ __forceinline__ float4 ldg(const float4* p) {
+    const f4v v = *(const g_f4v*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // ---- diagnostic statistics (stats variants only; never in a timed build) ----
 // Wave-level: the first active lane adds into the wave's LDS counters, so a
 // region is charged once per wave execution whatever its EXEC mask.
@@ -147,7 +160,7 @@ __device__ __forceinline__ float div_nr(float num, float den, float r) {
 // rcp_nr(a), unless a lane's a = dot(dir, dir) is below 2^-60.
 __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
                                          float tmax, float& t, bool fd = false, float ra = 0.0f) {
-    float4 A = sp[0], B = sp[1];
+    float4 A = ldg(sp), B = ldg(sp + 1);
     v3 center = add3(f3(A), scale3(f3(B), time));
     v3 oc = sub3(o, center);
     float half_b = g_dot(oc, d);
@@ -196,14 +209,14 @@ __device__ __forceinline__ bool face_interior(float4 A, float4 B, v3 o, v3 d, fl
 // hitting.glsl:90-133 without the record writes; f = dquads record.
 __device__ __forceinline__ bool quad_test(const float4* __restrict__ f, v3 o, v3 d, float tmin, float tmax, float& t,
                                           float& alpha, float& beta, bool fd = false) {
-    float4 Q0 = f[0];
+    float4 Q0 = ldg(f);
     v3 n = f3(Q0);
     float denom = g_dot(n, d);
     if (fabsf(denom) < 1e-8f) return false;
     const float num = Q0.w - g_dot(n, o);
     float tt = fd ? div_nr(num, denom, rcp_nr(denom)) : num / denom;
     if (!(tmin <= tt && tt <= tmax)) return false;
-    if (!face_interior(f[1], f[2], o, d, tt, alpha, beta, fd)) return false;
+    if (!face_interior(ldg(f + 1), ldg(f + 2), o, d, tt, alpha, beta, fd)) return false;
     t = tt;
     return true;
 }
@@ -223,7 +236,7 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
         unsigned cand = 0;
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            float4 pl = fb[h + k];
+            float4 pl = ldg(fb + h + k);
             v3 n = f3(pl);
             float denom = g_dot(n, d);
             ti[k] = (pl.w - g_dot(n, o)) / denom;   // unused when |denom| < 1e-8
@@ -234,7 +247,7 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
             const int i = h + k;
             if ((cand >> k) & 1u) {
                 float al, be;
-                if (ti[k] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[k], al, be, fd)) {
+                if (ti[k] <= tmax && face_interior(ldg(fb + 6 + 2 * i), ldg(fb + 7 + 2 * i), o, d, ti[k], al, be, fd)) {
                     tmax = ti[k];
                     t = ti[k];
                     face = i;
@@ -260,7 +273,7 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
 __device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, const float4* __restrict__ fb, v3 o,
                                                v3 d, float tmin, float tmax, float& t, int& face, float& alpha,
                                                float& beta, bool fd = false) {
-    const float4 c0 = pl[0], c1 = pl[1], c2 = pl[2];
+    const float4 c0 = ldg(pl), c1 = ldg(pl + 1), c2 = ldg(pl + 2);
     const float sv[6] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z};
     const float wv[6] = {c0.y, c0.w, c1.y, c1.w, c2.y, c2.w};
     const float dk[6] = {d.z, d.x, d.z, d.x, d.y, d.y};
@@ -292,7 +305,7 @@ __device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, co
     for (int i = 0; i < 6; i++) {
         if ((cand >> i) & 1u) {
             float al, be;
-            if (ti[i] <= tmax && face_interior(fb[6 + 2 * i], fb[7 + 2 * i], o, d, ti[i], al, be, fd)) {
+            if (ti[i] <= tmax && face_interior(ldg(fb + 6 + 2 * i), ldg(fb + 7 + 2 * i), o, d, ti[i], al, be, fd)) {
                 tmax = ti[i];
                 t = ti[i];
                 face = i;
@@ -521,7 +534,6 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
 // Node reads: an LDS address is the node's byte offset plus the dynamic region's
 // base, which is 0 in a kernel without static LDS (every non-stats build), so
 // the offset is the address itself (no add per step).
-typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const f4v lds_f4;
 template <bool EXACT, bool STATS>
 __device__ __forceinline__ uint32_t link_walk(const char* __restrict__ base, uint32_t nx, v3 o, v3 inv, float tmin,
@@ -693,9 +705,9 @@ __device__ __forceinline__ void texel(const rt_dtex& T, int x, int y, float out[
     if (!T.data || x < 0 || y < 0 || x >= T.w || y >= T.h) return;
     int i = y * T.w + x;
     if (T.is_float) {
-        out[0] = reinterpret_cast<const float*>(T.data)[i];
+        out[0] = ((g_f*)T.data)[i];
     } else {
-        uint32_t c = reinterpret_cast<const uint32_t*>(T.data)[i];
+        uint32_t c = ((__attribute__((address_space(1))) const uint32_t*)T.data)[i];
         out[0] = unorm8_fast(c & 0xFFu);
         out[1] = unorm8_fast((c >> 8) & 0xFFu);
         out[2] = unorm8_fast((c >> 16) & 0xFFu);
@@ -707,12 +719,15 @@ __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
     return t[0];
 }
 
-// texel_r of an R32F table given as a plain pointer (LDS copy or global)
+// texel_r of an R32F table: the LDS copy (ds_read) or the texture in global memory
+template <bool LDS>
 __device__ __forceinline__ float table_r(const float* tab, int w, int h, int x, int y) {
-    return (!tab || x < 0 || y < 0 || x >= w || y >= h) ? 0.0f : tab[y * w + x];
+    if (!tab || x < 0 || y < 0 || x >= w || y >= h) return 0.0f;
+    return LDS ? ((lds_f*)tab)[y * w + x] : ((g_f*)tab)[y * w + x];
 }
 
 // texture.glsl:38-77 with perlin_interp (19-36) fused; Hermite applied twice (Q6)
+template <bool LDS>
 __device__ __forceinline__ float perlin_noise(const float* tab, int tw, int th, v3 p) {
     float u = p.x - floorf(p.x);
     float v = p.y - floorf(p.y);
@@ -729,15 +744,15 @@ __device__ __forceinline__ float perlin_noise(const float* tab, int tw, int th, 
     float accum = 0.0f;
 #pragma unroll
     for (int di = 0; di < 2; di++) {
-        int px = rt_f2i(table_r(tab, tw, th, 3, (i + di) & 255));
+        int px = rt_f2i(table_r<LDS>(tab, tw, th, 3, (i + di) & 255));
 #pragma unroll
         for (int dj = 0; dj < 2; dj++) {
-            int py = rt_f2i(table_r(tab, tw, th, 4, (j + dj) & 255));
+            int py = rt_f2i(table_r<LDS>(tab, tw, th, 4, (j + dj) & 255));
 #pragma unroll
             for (int dk = 0; dk < 2; dk++) {
-                int pz = rt_f2i(table_r(tab, tw, th, 5, (k + dk) & 255));
+                int pz = rt_f2i(table_r<LDS>(tab, tw, th, 5, (k + dk) & 255));
                 int idx = px ^ py ^ pz;
-                v3 c = mk3(table_r(tab, tw, th, 0, idx), table_r(tab, tw, th, 1, idx), table_r(tab, tw, th, 2, idx));
+                v3 c = mk3(table_r<LDS>(tab, tw, th, 0, idx), table_r<LDS>(tab, tw, th, 1, idx), table_r<LDS>(tab, tw, th, 2, idx));
                 v3 wv = mk3(u - (float)di, v - (float)dj, w - (float)dk);
                 float fi = (float)di, fj = (float)dj, fk = (float)dk;
                 accum += (fi * uu + (1.0f - fi) * (1.0f - uu)) * (fj * vv + (1.0f - fj) * (1.0f - vv)) *
@@ -794,13 +809,13 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         if (P.debug_flags & 1) return mk3s(0.5f);   // ablation only (RT_DEBUG_FLAGS), never exact
         float scale = ((float)detail_i / 4095.0f) * 100.0f;
         float accum = 0.0f, weight = 1.0f;
-        const float* tab = (P.perlin_lds >= 0 && (index & 7) == P.perlin_slot)
-                               ? reinterpret_cast<const float*>(rt_dyn_lds + P.perlin_lds)
+        const bool lds = P.perlin_lds >= 0 && (index & 7) == P.perlin_slot;
+        const float* tab = lds ? reinterpret_cast<const float*>(rt_dyn_lds + P.perlin_lds)
                                : reinterpret_cast<const float*>(T.is_float ? T.data : nullptr);
         v3 q = p;
 #pragma unroll 1
         for (int o = 0; o < 7; o++) {
-            accum += weight * perlin_noise(tab, T.w, T.h, q);
+            accum += weight * (lds ? perlin_noise<true>(tab, T.w, T.h, q) : perlin_noise<false>(tab, T.w, T.h, q));
             weight *= 0.5f;
             q = scale3(q, 2.0f);
         }
@@ -1212,7 +1227,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     v3 emis = mk3s(0.0f);
     if (h.type == RT_MODEL_SPHERE) {   // hitting.glsl:40-42 + compute.glsl:199-204
         const float4* sp = reinterpret_cast<const float4*>(P.spheres + h.idx);
-        float4 A = sp[0], B = sp[1], C = sp[2];
+        float4 A = ldg(sp), B = ldg(sp + 1), C = ldg(sp + 2);
         v3 center = add3(f3(A), scale3(f3(B), S.time));
         v3 on = divs3(sub3(p, center), B.w);
         front = g_dot(d, on) < 0.0f;
@@ -1228,12 +1243,12 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     } else {   // quad, or box face h.face (material from quads[0], compute.glsl:217-221)
         const float4* q0 = (h.type == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + h.idx)
                                                     : reinterpret_cast<const float4*>(P.boxes + h.idx);
-        v3 n = f3(q0[5 * h.face]);
+        v3 n = f3(ldg(q0 + 5 * h.face));
         front = g_dot(d, n) < 0.0f;
         normal = front ? n : neg3(n);
-        material = __float_as_int(q0[1].w);
-        tex_id = __float_as_int(q0[2].w);
-        if (front) emis = f3(q0[4]);
+        material = __float_as_int(ldg(q0 + 1).w);
+        tex_id = __float_as_int(ldg(q0 + 2).w);
+        if (front) emis = f3(ldg(q0 + 4));
     }
     // scatter (scatter.glsl:43-98)
     int mid = (material >> 16) & 0xFFFF;
