@@ -19,6 +19,13 @@
 // MI355X-only options (no reference counterpart): --seed (scene + per-frame
 // factor seed; the reference uses the unseeded Math.random), --devices
 // (comma-separated HIP device ids, rows striped across them), --frames-per-launch.
+//
+// Progressive preview, the headless form of the window loop
+// (Window.java:250-281): --preview <png> rewrites that PNG with the running mean
+// every --preview-every frames (drawResult: the image so far, through
+// Texture.saveAsPNG) and prints GuiRenderer.draw's status lines
+// (GuiRenderer.java:48-62): "Last raytrace took: <ms> ms." and
+// "Sample: <n>/<spp>." (+ "Render completed in: ..." once complete).
 #include "rt/rt.h"
 #include "rt/rt_scene.h"
 
@@ -44,7 +51,7 @@ struct Opt {
 };
 
 // commons-cli Options in Main.getOptions order (Main.java:43-70)
-enum { O_HELP, O_SCENE, O_RES, O_SPP, O_DEPTH, O_OUT, O_SEED, O_DEVICES, O_PER_LAUNCH, O_N };
+enum { O_HELP, O_SCENE, O_RES, O_SPP, O_DEPTH, O_OUT, O_SEED, O_DEVICES, O_PER_LAUNCH, O_PREVIEW, O_PREVIEW_EVERY, O_N };
 const Opt kOpts[O_N] = {
     {"h", "help", false, "print help message"},
     {"s", "scene", true, "scene ID"},
@@ -56,6 +63,8 @@ const Opt kOpts[O_N] = {
     {nullptr, "seed", true, "scene and frame RNG seed (default 1)"},
     {nullptr, "devices", true, "comma-separated HIP device ids (default 0)"},
     {nullptr, "frames-per-launch", true, "frames per kernel launch (default 64)"},
+    {nullptr, "preview", true, "progressive preview PNG, rewritten every --preview-every frames"},
+    {nullptr, "preview-every", true, "frames between preview updates (default: --frames-per-launch)"},
 };
 
 // HelpFormatter.printHelp("OpenGL Ray Tracer", options): options sorted by key.
@@ -204,6 +213,9 @@ int main(int argc, char** argv) {
         uncaught("java.lang.IllegalArgumentException", "Invalid scene ID: " + std::to_string(scene_id));
     if (width <= 0 || height <= 0) die("rtrender", "resolution must be positive");
     if (per_launch <= 0) die("rtrender", "--frames-per-launch must be positive");
+    const std::string preview = get(O_PREVIEW, nullptr);
+    const int preview_every = seen[O_PREVIEW_EVERY] ? parse_int(val[O_PREVIEW_EVERY]) : per_launch;
+    if (preview_every <= 0) die("rtrender", "--preview-every must be positive");
 
     rts_scene* scene = nullptr;
     if (rts_build(scene_id, width, height, (uint64_t)seed, nullptr, &scene) != 0) die("rts_build", rts_last_error());
@@ -241,14 +253,33 @@ int main(int argc, char** argv) {
     auto t0 = std::chrono::steady_clock::now();
     std::vector<float> rf((size_t)per_launch);
     uint64_t device_ns = 0;
-    for (int f0 = 0; f0 < spp; f0 += per_launch) {
+    std::vector<float> rgba;
+    for (int f0 = 0; f0 < spp;) {
         int n = std::min(per_launch, spp - f0);
+        if (!preview.empty()) n = std::min(n, preview_every - f0 % preview_every);   // stop at the next preview
         for (int i = 0; i < n; i++) rf[i] = rt_frame_rand_factor((uint64_t)seed, (uint64_t)(f0 + i));
         chk(rt_render(ctx, f0 + 1, n, rf.data()), "rt_render");
         chk(rt_sync(ctx), "rt_sync");
         uint64_t ns = 0;
         chk(rt_last_render_ns(ctx, &ns), "rt_last_render_ns");
         device_ns += ns;
+        f0 += n;
+        if (!preview.empty() && (f0 % preview_every == 0 || f0 == spp)) {
+            // one pass of the window loop: drawResult + GuiRenderer.draw
+            rgba.resize((size_t)width * height * 4);
+            chk(rt_read_image(ctx, rgba.data()), "rt_read_image");
+            if (rts_save_png(rgba.data(), width, height, preview.c_str()) != 0)
+                uncaught("java.lang.RuntimeException", "Failed to save texture as PNG");
+            std::printf("Last raytrace took: %d ms.\n", (int)(ns / 1000000));
+            std::printf("Sample: %d/%d.", f0, spp);
+            if (f0 == spp) {
+                const int ms = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
+                                   std::chrono::steady_clock::now() - t0).count();
+                std::printf("Render completed in: %s.", finish_time_string(ms).c_str());
+            }
+            std::printf("\n");
+            std::fflush(stdout);
+        }
     }
     int finish_ms = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
                         std::chrono::steady_clock::now() - t0).count();

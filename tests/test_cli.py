@@ -107,6 +107,28 @@ def test_png_is_saveAsPNG_of_the_oracle_image(gpu, tmp_path, sid, devices, per_l
     assert np.array_equal(read_png(out), rtamd.tonemap_rgb8(ref))
 
 
+@pytest.mark.gpu
+def test_progressive_preview(gpu, tmp_path):
+    """--preview: the headless window loop (Window.java:250-281).  Every
+    --preview-every frames the preview PNG holds the running mean so far (checked
+    against the oracle after 3 of 8 frames) and GuiRenderer.draw's status lines are
+    printed; at the end it equals the -o output."""
+    w, h, spp = 64, 48, 8
+    prev, out = tmp_path / "preview.png", tmp_path / "out.png"
+    r = run("-s", 9, "-r", f"{w}:{h}", "-spp", 3, "-md", 5, "--preview", prev, "--preview-every", 3)
+    assert r.returncode == 0, r.stderr
+    assert "Sample: 3/3.Render completed in: " in r.stdout
+    sc = rtamd.Scene(9, w, h, seed=1)
+    assert np.array_equal(read_png(prev), rtamd.tonemap_rgb8(oracle_image(sc, 3, max_depth=5, spp=3)))
+    r = run("-s", 9, "-r", f"{w}:{h}", "-spp", spp, "-md", 5, "-o", out, "--preview", prev, "--preview-every", 3,
+            "--frames-per-launch", 2)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("Sample: ")]
+    assert [l.split(".")[0] for l in lines] == ["Sample: 3/8", "Sample: 6/8", "Sample: 8/8"], lines
+    assert r.stdout.count("Last raytrace took: ") == 3
+    assert np.array_equal(read_png(prev), read_png(out))
+
+
 @pytest.mark.parametrize("ms,text", [(3723456, "1hour 2minutes 3.456seconds"), (59999, "59.999seconds"),
                                      (61005, "1minutes 1.5seconds"), (0, "0.0seconds")])
 def test_finish_time_string(ms, text):

@@ -78,15 +78,18 @@ def main():
             if r.returncode in (124, 134, 137, 139):
                 break
             continue
+        # sum a counter over this pass's rows (dimensions / XCDs); a counter that an
+        # earlier group already measured keeps that pass's value (never summed across passes)
+        got = {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     if "render_" not in row.get("Kernel_Name", ""):
                         continue
                     name = row.get("Counter_Name")
-                    val = float(row.get("Counter_Value", 0))
-                    res.setdefault(name, 0.0)
-                    res[name] += val
+                    got[name] = got.get(name, 0.0) + float(row.get("Counter_Value", 0))
+        for name, val in got.items():
+            res.setdefault(name, val)
     # per launch (render_once --launches 1 => one render dispatch per pass)
     if "FETCH_SIZE" in res:
         res["hbm_read_bytes_raw"] = res["FETCH_SIZE"] * 1024
