@@ -102,6 +102,8 @@ struct rt_ctx {
     bool boxes_canon = false;   // every box has Box.java's axis-aligned face layout (dboxes[18..20])
     bool fd_ok[6] = {true, true, true, true, true, true};   // per binding: records in the fast-division regime
     bool fd_cam = true;
+    bool boxes_axis = false;   // every box face's u and v lie along one axis each (box pre-test)
+    float scene_extent = -1.0f;   // max |coordinate| over records and camera (< 0: not computed)
     bool validated = false;
     uint64_t last_ns = 0;
     int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
@@ -116,6 +118,7 @@ struct rt_ctx {
     int chunk_target = 32;
     int stage_tiles = 4;
     bool fastdiv = true;   // shared-reciprocal divisions where exact (env RT_FASTDIV=0 disables; A/B)
+    bool box_pretest = true;   // the canonical box tests' bounds pre-test (env RT_BOX_PRETEST=0 disables; A/B)
     int sm_batch = 64;   // render_sm's shading batch (env RT_SM_BATCH) ...
     int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
     int walk_frac = 48;  // render_sm: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
@@ -630,6 +633,30 @@ bool fd_face(const float4 f[3]) {
            fd_coord(f[2].x) && fd_coord(f[2].y) && ad >= 0x1p-60f && ad <= 0x1p20f;
 }
 
+// Max |coordinate| a ray origin or hit point can have: every record's reach (sphere
+// centre + motion + radius, quad / box corners) and the camera block.
+float scene_extent(const rt_ctx* c) {
+    double b = 0.0;
+    const auto& S = c->host_buf[RT_BIND_SPHERES];
+    for (size_t k = 0; k < S.size() / sizeof(rt_sphere); k++) {
+        const rt_sphere& sp = ((const rt_sphere*)S.data())[k];
+        for (int i = 0; i < 3; i++)
+            b = std::max(b, std::fabs((double)sp.center1[i]) + std::fabs((double)sp.center_vec[i]) +
+                                std::fabs((double)sp.radius));
+    }
+    for (int bind : {RT_BIND_QUADS, RT_BIND_BOXES}) {
+        const auto& Q = c->host_buf[bind];
+        for (size_t k = 0; k < Q.size() / sizeof(rt_quad); k++) {
+            const rt_quad& q = ((const rt_quad*)Q.data())[k];
+            for (int i = 0; i < 3; i++)
+                b = std::max(b, std::fabs((double)q.q[i]) + std::fabs((double)q.u[i]) + std::fabs((double)q.v[i]));
+        }
+    }
+    const float* cam = (const float*)&c->cam;
+    for (int i = 0; i < 28; i++) b = std::max(b, std::fabs((double)cam[i]));
+    return b < 1e30 ? (float)b : INFINITY;
+}
+
 int validate(rt_ctx* c) {
     if (c->validated) return RT_OK;
     size_t ns = c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere);
@@ -734,6 +761,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("RT_STAGE_TILES")) c->stage_tiles = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("RT_FASTDIV")) c->fastdiv = std::atoi(v) != 0;
+    if (const char* v = std::getenv("RT_BOX_PRETEST")) c->box_pretest = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_SM_BATCH")) c->sm_batch = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SM_FRAC")) c->sm_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_WALK_FRAC")) c->walk_frac = std::max(1, std::min(64, std::atoi(v)));
@@ -806,6 +834,7 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
     H.assign((const uint8_t*)bytes, (const uint8_t*)bytes + nbytes);
     c->uploaded[binding] = true;
     c->validated = false;
+    c->scene_extent = -1.0f;
     if (binding == RT_BIND_BVH) {
         c->n_dnodes = (int)dn.size();
         c->spec_ok = boxes_nest(dn);
@@ -826,9 +855,28 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
             // per box: the 6 planes first, then the 6 (A, B) pairs, then the canonical
             // planes (RT_DBOX_F4 float4)
             c->boxes_canon = true;
+            c->boxes_axis = true;
             for (size_t bx = 0; bx < nq / 6; bx++) {
                 float4* o = &faces[bx * RT_DBOX_F4];
                 float sw[12];
+                double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                for (int i = 0; i < 6; i++) {   // the bounds: every face's corners
+                    const rt_quad& Q = qs[bx * 6 + i];
+                    int nz_u = 0, nz_v = 0;
+                    for (int k = 0; k < 3; k++) {
+                        nz_u += Q.u[k] != 0.0f;
+                        nz_v += Q.v[k] != 0.0f;
+                        for (int cu = 0; cu < 2; cu++)
+                            for (int cv = 0; cv < 2; cv++) {
+                                const double x = (double)Q.q[k] + cu * (double)Q.u[k] + cv * (double)Q.v[k];
+                                lo[k] = std::min(lo[k], x);
+                                hi[k] = std::max(hi[k], x);
+                            }
+                    }
+                    if (nz_u != 1 || nz_v != 1) c->boxes_axis = false;
+                }
+                o[21] = make_float4((float)lo[0], (float)hi[0], (float)lo[1], (float)hi[1]);
+                o[22] = make_float4((float)lo[2], (float)hi[2], 0.0f, 0.0f);
                 for (int i = 0; i < 6; i++) {
                     float4 f[3];
                     face_record(qs[bx * 6 + i], f);
@@ -920,6 +968,7 @@ int rt_set_camera(rt_ctx* c, const float ubo[28]) {
     if (!c || !ubo) return set_err(c, RT_ERR_INVALID_ARG, "NULL camera");
     std::memcpy(&c->cam, ubo, sizeof(rt_camera_ubo));
     c->have_cam = true;
+    c->scene_extent = -1.0f;
     c->fd_cam = true;   // the camera's points and vectors within the fast-division regime's 2^20
     for (int i = 0; i < 28; i++) c->fd_cam = c->fd_cam && fd_coord(ubo[i]);
     return RT_OK;
@@ -1020,6 +1069,15 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.lights_count = lc;
     a.uv_always = c->uv_always;
     a.boxes_canon = c->boxes_canon ? 1 : 0;
+    // Box pre-test (rt_kernel.hip leaf_prims_t): a face the exact test accepts lies, with
+    // the ray's point at its t, within ~2^-20 of the scene's extent of the box (the face
+    // tests' rounding); the kernel's slab test of the box grown by 2^-13 of that extent
+    // cannot miss it.  Needs axis-aligned faces (the face test then measures the point
+    // along the box's own axes).
+    if (c->scene_extent < 0.0f) c->scene_extent = scene_extent(c);
+    a.box_margin = (c->boxes_canon && c->boxes_axis && c->box_pretest && c->scene_extent <= 0x1p60f)
+                       ? std::max(c->scene_extent, 1.0f) * 0x1p-13f
+                       : 0.0f;
     a.fastdiv = (c->fastdiv && c->fd_cam && c->fd_ok[RT_BIND_SPHERES] && c->fd_ok[RT_BIND_QUADS] &&
                  c->fd_ok[RT_BIND_BOXES])
                     ? 1

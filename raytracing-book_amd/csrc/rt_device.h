@@ -9,7 +9,8 @@
 //   dquads   : per quad RT_DFACE_F4 float4: plane (n, d), A = (q_a, q_b, u_a, u_b),
 //              B = (v_a, v_b, delta, axis case) — the intersection-only face record
 //   dboxes   : per box RT_DBOX_F4 float4: the 6 planes, then the 6 (A, B) pairs, then the
-//              canonical planes (s_i, w_i) x 6 in 3 float4 (boxes_canon, below)
+//              canonical planes (s_i, w_i) x 6 in 3 float4 (boxes_canon, below), then the
+//              box's bounds (xmin, xmax, ymin, ymax), (zmin, zmax, 0, 0) (box_margin)
 //   media    : rt_medium[] as uploaded (20 B)
 //   lights   : int32 packed ids
 //   textures : RGB8 expanded to RGBA8 (4 B/texel, aligned), RGBA8, R32F
@@ -28,7 +29,7 @@
 #define RT_MAX_FRAMES_PER_LAUNCH 256
 #define RT_NODE_END 0xFFFFu
 #define RT_DFACE_F4 3    // float4 per dquads record
-#define RT_DBOX_F4 21    // float4 per dboxes record
+#define RT_DBOX_F4 23    // float4 per dboxes record
 // LDS per 512-thread workgroup (2 workgroups per CU share 160 KiB): what the
 // launch shape stages (at most RT_LDS_DYN_BYTES), then the lanes' running-mean
 // slots (RT_LDS_ACC_BYTES), all in the dynamic region (no static LDS)
@@ -106,6 +107,9 @@ struct rt_kernel_args {
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
     int fastdiv;                 // the scene's records are in the shared-reciprocal division regime
+    float box_margin;            // > 0: canonical box tests start with a slab test of the box's bounds
+                                 // grown by this margin (2^-13 of the scene's extent), which no face
+                                 // the exact test accepts can lie outside; 0: no pre-test
     int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1
     int perlin_lds;              // its float4 offset in the dynamic LDS (after the nodes), or -1
     int n_media;

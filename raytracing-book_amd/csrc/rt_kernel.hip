@@ -476,7 +476,7 @@ __device__ __forceinline__ bool aabb_pk(float4 n0, float4 n1, v3 o, v3 inv, floa
 // The two prims of a leaf (compute.glsl:247-256), left then right.
 // FD: the shared-reciprocal divisions (rcp_nr / div_nr; FD kernels only).
 template <bool STATS, bool FD>
-__device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, float a,
+__device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, v3 inv, float a,
                                              float time, float tmin, float& tmax, float& rf, float px, float py, Hit& h,
                                              bool& has, unsigned long long* st) {
     constexpr bool fd = FD;
@@ -507,9 +507,19 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_QUAD_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_BOX) {
-            hit = (P.boxes_canon && fin) ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix + 18, P.dboxes + RT_DBOX_F4 * ix, o,
-                                                          d, tmin, tmax, t, face, al, be, fd)
-                                         : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be, fd);
+            const float4* rec = P.dboxes + RT_DBOX_F4 * ix;
+            bool maybe = true;
+            if (P.box_margin > 0.0f && P.boxes_canon && fin) {
+                // the box's bounds grown by box_margin (rt_device.h): a ray that misses them
+                // misses every face the exact test below would accept
+                const float m = P.box_margin;
+                const float4 b0 = ldg(rec + 21), b1 = ldg(rec + 22);
+                maybe = aabb_pk(make_float4(b0.x - m, b0.y + m, b0.z - m, b0.w + m),
+                                make_float4(b1.x - m, b1.y + m, 0.0f, 0.0f), o, inv, tmin, tmax);
+            }
+            if (maybe)
+                hit = (P.boxes_canon && fin) ? box_test_canon(rec + 18, rec, o, d, tmin, tmax, t, face, al, be, fd)
+                                             : box_test(rec, o, d, tmin, tmax, t, face, al, be, fd);
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
@@ -642,7 +652,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
             unsigned long long t1 = STATS ? clock64() : 0;
             if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
             const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
-            leaf_prims_t<STATS, false>(P, lf.x, lf.y, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+            leaf_prims_t<STATS, false>(P, lf.x, lf.y, o, d, inv, a, time, tmin, tmax, rf, px, py, h, has, st);
             if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
             nx &= 0xFFFFu;
             if (nx == 0xFFFFu) break;
@@ -682,7 +692,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
         if (!leaf) break;
         unsigned long long t1 = STATS ? clock64() : 0;
         if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-        leaf_prims_t<STATS, false>(P, meta, prims, o, d, a, time, tmin, tmax, rf, px, py, h, has, st);
+        leaf_prims_t<STATS, false>(P, meta, prims, o, d, inv, a, time, tmin, tmax, rf, px, py, h, has, st);
         if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
     }
     return has;
@@ -1649,8 +1659,8 @@ __device__ __forceinline__ void render_sm(const KP& P, const float4* __restrict_
                     unsigned long long t1 = STATS ? clock64() : 0;
                     if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
                     const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
-                    leaf_prims_t<STATS, FD>(P, lf.x, lf.y, S.o, S.d, a, S.time, 0.001f, tmax, S.rf, fx, fy, h, has,
-                                            st);
+                    leaf_prims_t<STATS, FD>(P, lf.x, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf, fx, fy, h,
+                                            has, st);
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
                     nx &= 0xFFFFu;
                     if (nx == 0xFFFFu) status = RT_SM_HIT;
