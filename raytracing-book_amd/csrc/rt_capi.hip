@@ -109,13 +109,15 @@ struct rt_ctx {
     int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
     int variant_no_stats = -1;   // the variant active before rt_debug_enable_stats(c, 1), restored by (c, 0)
     // Work split: aim for chunk_target work units per resident wave (env
-    // RT_CHUNK_TARGET; 0 = one chunk per tile).  With at least stage_tiles tiles
+    // RT_CHUNK_TARGET; 0 = one chunk per tile), staged_chunk_target when staged
+    // (RT_STAGED_CHUNK_TARGET).  With at least stage_tiles tiles
     // per resident wave (env RT_STAGE_TILES) the chunks are ordered (the running
     // mean is handed from wave to wave, rt_kernel.hip wait_chunk); with fewer, a
     // tile's frames would be one long serial chain, so the chunks run in parallel,
     // stage their per-frame colours (at most sample_budget bytes) and fold_kernel
     // applies the running mean in frame order.
-    int chunk_target = 32;
+    int chunk_target = 16;          // ordered chunks (RT_CHUNK_TARGET)
+    int staged_chunk_target = 32;   // staged chunks (RT_STAGED_CHUNK_TARGET)
     int stage_tiles = 4;
     bool fastdiv = true;   // shared-reciprocal divisions where exact (env RT_FASTDIV=0 disables; A/B)
     bool box_pretest = true;   // the canonical box tests' bounds pre-test (env RT_BOX_PRETEST=0 disables; A/B)
@@ -760,6 +762,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     }
     if (const char* v = std::getenv("RT_CHUNK_TARGET")) c->chunk_target = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("RT_STAGE_TILES")) c->stage_tiles = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("RT_STAGED_CHUNK_TARGET")) c->staged_chunk_target = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("RT_FASTDIV")) c->fastdiv = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_BOX_PRETEST")) c->box_pretest = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_SM_BATCH")) c->sm_batch = std::max(1, std::min(64, std::atoi(v)));
@@ -1184,11 +1187,12 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         int per_launch = RT_MAX_FRAMES_PER_LAUNCH;
         int chunks_wanted = 1;
         const long long waves = rt_resident_waves();
+        const bool few_tiles = (long long)n_tiles < (long long)c->stage_tiles * waves;
         if (c->chunk_target > 0 && n_tiles > 0) {
-            chunks_wanted = (int)std::min<long long>(RT_MAX_FRAMES_PER_LAUNCH,
-                                                     (c->chunk_target * waves + n_tiles - 1) / n_tiles);
+            const long long target = few_tiles ? c->staged_chunk_target : c->chunk_target;
+            chunks_wanted = (int)std::min<long long>(RT_MAX_FRAMES_PER_LAUNCH, (target * waves + n_tiles - 1) / n_tiles);
         }
-        const bool staged = chunks_wanted > 1 && (long long)n_tiles < (long long)c->stage_tiles * waves;
+        const bool staged = chunks_wanted > 1 && few_tiles;
         const size_t n_pixels = (size_t)d.local_rows * c->width;
         if (staged) {
             const size_t per_frame = n_pixels * sizeof(float4);

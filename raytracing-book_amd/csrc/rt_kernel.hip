@@ -76,7 +76,9 @@ enum {
     ST_SPH_CYC, ST_QUAD_CYC, ST_BOX_CYC, ST_MED_CYC,
     // link walk: traces begun (wave calls, lanes), and rounds of its node-walk + leaf loop with the
     // lanes whose trace is still running (the rest wait for the wave's longest trace)
-    ST_TRACE_IT, ST_TRACE_LN, ST_ROUND_IT, ST_ROUND_LN, ST_N
+    ST_TRACE_IT, ST_TRACE_LN, ST_ROUND_IT, ST_ROUND_LN,
+    // render_sm rounds: lanes of the wave already retired (their unit has no samples left)
+    ST_RET_IT, ST_RET_LN, ST_N
 };
 __device__ __forceinline__ bool first_active_lane() {
     unsigned long long m = __ballot(1);
@@ -1636,6 +1638,7 @@ __device__ __forceinline__ void render_sm(const KP& P, const float4* __restrict_
         for (;;) {
             const unsigned long long tr = __ballot(status == RT_SM_TRACE);
             const int n_hit = __popcll(__ballot(status == RT_SM_HIT));
+            if (STATS && tr) st_pred(st, status == RT_SM_RETIRED, ST_RET_IT, ST_RET_LN);
             if (tr == 0 || n_hit >= batch || n_hit * 64 >= P.sm_frac * (n_hit + __popcll(tr))) break;
             const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
             const bool wave_exact = __ballot(status == RT_SM_TRACE && lane_exact) != 0;

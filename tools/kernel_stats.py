@@ -14,7 +14,8 @@ NAMES = ["TOTAL", "START_CYC", "START_IT", "START_LN", "NODE_CYC", "NODE_IT", "N
          "LEAF_LN", "SPH_LN", "QUAD_LN", "BOX_LN", "MED_LN", "SHADE_CYC", "SHADE_IT", "SHADE_LN", "SPH_IT",
          "QUAD_IT", "BOX_IT", "MED_IT", "FAST_TRACES", "FAST_EXACT"] + [f"FAST_WHY{r}" for r in range(1, 10)] + [
          "FAST_STEPS", "FAST_TESTS", "FAST_PRE_CYC", "FAST_POST_CYC", "FAST_EXACT_CYC",
-         "SPH_CYC", "QUAD_CYC", "BOX_CYC", "MED_CYC", "TRACE_IT", "TRACE_LN", "ROUND_IT", "ROUND_LN"]
+         "SPH_CYC", "QUAD_CYC", "BOX_CYC", "MED_CYC", "TRACE_IT", "TRACE_LN", "ROUND_IT", "ROUND_LN",
+         "RET_IT", "RET_LN"]
 
 
 def main():
@@ -54,6 +55,9 @@ def main():
         print(f"  link walk: {v['TRACE_LN'] / v['TRACE_IT']:5.2f} lanes per wave trace, "
               f"{v['ROUND_IT'] / v['TRACE_IT']:5.2f} node-walk+leaf rounds per wave trace, "
               f"{v['ROUND_LN'] / (64.0 * max(v['ROUND_IT'], 1)) * 100:5.1f}% of lanes still tracing per round")
+    if v["ROUND_IT"]:
+        print(f"  rounds with retired lanes: {v['RET_IT'] / v['ROUND_IT'] * 100:5.1f}% of rounds, "
+              f"{v['RET_LN'] / (64.0 * v['ROUND_IT']) * 100:5.1f}% of lane-rounds retired (unit tails)")
     print("raw", v)
 
 
