@@ -115,16 +115,18 @@ struct rt_ctx {
     // mean is handed from wave to wave, rt_kernel.hip wait_chunk); with fewer, a
     // tile's frames would be one long serial chain, so the chunks run in parallel,
     // stage their per-frame colours (at most sample_budget bytes) and fold_kernel
-    // applies the running mean in frame order.
+    // applies the running mean in frame order.  The default stage_tiles stages
+    // every chunked launch: with render_stream that measured fastest at N = 1 too
+    // (scene 8 -5% against ordered chunks).
     int chunk_target = 16;          // ordered chunks (RT_CHUNK_TARGET)
-    int staged_chunk_target = 32;   // staged chunks (RT_STAGED_CHUNK_TARGET)
-    int stage_tiles = 4;
+    int staged_chunk_target = 48;   // staged chunks (RT_STAGED_CHUNK_TARGET)
+    int stage_tiles = 1 << 20;      // in effect always staged (the measured best with render_stream)
     bool fastdiv = true;   // shared-reciprocal divisions where exact (env RT_FASTDIV=0 disables; A/B)
     bool box_pretest = true;   // the canonical box tests' bounds pre-test (env RT_BOX_PRETEST=0 disables; A/B)
     int sm_batch = 64;   // render_sm's shading batch (env RT_SM_BATCH) ...
     int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
     int walk_frac = 48;  // render_sm: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
-    size_t sample_budget = (size_t)16 << 30;
+    size_t sample_budget = (size_t)32 << 30;
 };
 
 namespace {
@@ -753,10 +755,11 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
         return fail(RT_ERR_INVALID_ARG, "rt_create: bad device count");
     rt_ctx* c = new rt_ctx();
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) {
-        // 0 = 37 (default), 30, 61 and their stats twins 38, 31, 69; anything else is the default
+        // 0 (default), 43, 40, 37, 30, 61 and their stats twins 39, 44, 41, 38, 31, 69
+        // (rt_kernel.hip rt_launch_render); anything else is the default
         const int want = std::atoi(v);
         c->variant = (want == 30 || want == 31 || want == 37 || want == 38 || want == 39 || want == 40 || want == 41 ||
-                      want == 61 || want == 69)
+                      want == 43 || want == 44 || want == 61 || want == 69)
                          ? want
                          : 0;
     }
@@ -1232,9 +1235,10 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             else if (staged) a.samples = (float4*)d.samples.ptr;
             a.wbuf = nullptr;
             a.wbuf_waves = 0;
-            if (!a.samples && (c->variant == 0 || c->variant == 39 || c->variant == 40 || c->variant == 41)) {
-                // pooled units fold per wave
-                const size_t need = (size_t)waves * 64 * (size_t)a.chunk_frames * sizeof(float4);
+            if (!a.samples && (c->variant == 0 || c->variant == 39 || c->variant == 40 || c->variant == 41 ||
+                               c->variant == 43 || c->variant == 44)) {
+                // pooled units fold per wave; two slots per wave (render_stream keeps two units in flight)
+                const size_t need = (size_t)waves * 2 * 64 * (size_t)a.chunk_frames * sizeof(float4);
                 if (d.wbuf.bytes < need) {
                     dev_free(d.wbuf);
                     HIPCHK(c, hipMalloc(&d.wbuf.ptr, need));
@@ -1269,7 +1273,8 @@ int rt_sync(rt_ctx* c) {
             HIPCHK(c, hipMemcpy(&fault, (unsigned*)d.counter.ptr + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
             if (fault) {
                 HIPCHK(c, hipMemset((unsigned*)d.counter.ptr + 1, 0, sizeof(unsigned)));
-                return set_err(c, RT_ERR_DEVICE, "render kernel: ordered-chunk wait timed out");
+                return set_err(c, RT_ERR_DEVICE, fault == 2 ? "render kernel: a wave exceeded its time bound"
+                                                            : "render kernel: ordered-chunk wait timed out");
             }
         }
     }
@@ -1450,6 +1455,7 @@ static int stats_twin(int v) {
     if (v == 30 || v == 31) return 31;
     if (v == 37 || v == 38) return 38;
     if (v == 40 || v == 41) return 41;
+    if (v == 43 || v == 44) return 44;
     return 39;
 }
 

@@ -40,6 +40,7 @@ typedef rt_kernel_args KP;
 #define RT_OPT_POOL 1   // pooled units (render_pool): without it a lane owns a pixel (variant 37)
 #define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_sm)
 #define RT_OPT_FD 4     // with RT_OPT_SM: the scene is in the shared-reciprocal division regime (P.fastdiv)
+#define RT_OPT_STREAM 8 // with RT_OPT_SM: the wave streams over units (render_stream) instead of one at a time
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -1598,9 +1599,21 @@ __device__ __forceinline__ void render_sm(const KP& P, const float4* __restrict_
                 if (s >= total) {
                     status = RT_SM_RETIRED;
                 } else {
-                    const uint32_t fl = s / nv, p = s - fl * nv;
-                    const int lr = ly0 + (int)(p / (uint32_t)wt), x = tx0 + (int)(p % (uint32_t)wt);
-                    const int y = ((lr / P.stripe_rows) * P.world + P.rank) * P.stripe_rows + lr % P.stripe_rows;
+                    uint32_t fl, py, px;
+                    if (nv == 64) {   // a full tile: shifts
+                        fl = s >> 6;
+                        py = (s >> 3) & 7u;
+                        px = s & 7u;
+                    } else {
+                        fl = s / nv;
+                        const uint32_t p = s - fl * nv;
+                        py = p / (uint32_t)wt;
+                        px = p - py * (uint32_t)wt;
+                    }
+                    const int lr = ly0 + (int)py, x = tx0 + (int)px;
+                    const int y = P.world == 1 ? lr
+                                               : ((lr / P.stripe_rows) * P.world + P.rank) * P.stripe_rows +
+                                                     lr % P.stripe_rows;
                     fx = (float)x;
                     fy = (float)y;
                     unsigned long long t0 = STATS ? clock64() : 0;
@@ -1731,6 +1744,272 @@ __device__ __forceinline__ void publish_chunk(const KP& P, int tile, int chunk) 
     __hip_atomic_store((gu32*)(P.tile_done + tile), (unsigned)(chunk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// render_sm over a stream of units (RT_OPT_STREAM): when the wave's current unit
+// has no unclaimed samples left, the wave claims its next unit and its free lanes
+// take that unit's samples while the other lanes finish the previous unit's paths
+// (before, they idled through the unit's tail: 8.5% of lane-rounds on scene 8).
+// Ordered / one-chunk launches keep up to two units in flight, each with its slot
+// of wbuf (2 per wave); a unit is folded into the image once all its samples are
+// stored, oldest first, so a wave only ever waits (wait_chunk) for units claimed
+// before its oldest one and the waits cannot form a cycle.  Staged launches store
+// straight to P.samples and need no slots.  A lane's sample is its pixel (fx, fy),
+// its slot `up` and its colour's place `dst` (slot offset frame-in-chunk * 64 +
+// pixel slot, or the staged index).
+struct UnitGeo {
+    int chunk, tile, tx0, ly0, wt, ht, f0, f1;
+    uint32_t total;
+};
+__device__ __forceinline__ UnitGeo unit_geo(const KP& P, int u, int n_tiles, int tiles_x) {
+    UnitGeo g;
+    g.chunk = u / n_tiles;
+    g.tile = u - g.chunk * n_tiles;
+    g.tx0 = (g.tile % tiles_x) * 8;
+    g.ly0 = (g.tile / tiles_x) * 8;
+    g.wt = min(8, P.width - g.tx0);
+    g.ht = min(8, P.local_rows - g.ly0);
+    g.f0 = g.chunk * P.chunk_frames;
+    g.f1 = min(P.n_frames, g.f0 + P.chunk_frames);
+    g.total = (uint32_t)(g.wt * g.ht * (g.f1 - g.f0));
+    return g;
+}
+template <bool STATS, int OPT, bool FD>
+__device__ __forceinline__ void render_stream(const KP& P, const float4* __restrict__ nodes, int gwave,
+                                              unsigned long long* st) {
+    const int lane = threadIdx.x & 63;
+    const bool staged = P.samples != nullptr;
+    const int tiles_x = (P.width + 7) >> 3;
+    const int n_tiles = tiles_x * ((P.local_rows + 7) >> 3);
+    const int n_units = n_tiles * P.n_chunks;
+    const uint32_t slot_f4 = 64u * (uint32_t)P.chunk_frames;
+    float4* const wbase = staged ? nullptr : P.wbuf + (size_t)gwave * 2 * slot_f4;
+    const rt_camera_ubo& C = P.cam;
+    const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
+    const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
+    const int batch = P.sm_batch;
+    // wave-uniform: the units in the two slots (-1 = free) and their stored samples;
+    // the pool: its unit, slot and next unclaimed sample
+    int unit0 = -1, unit1 = -1;
+    uint32_t done0 = 0, done1 = 0;
+    int cur = 1;
+    uint32_t next = 0, total_cur = 0;
+    bool no_more = false;
+    UnitGeo gc = unit_geo(P, 0, n_tiles, tiles_x);   // the pool unit's geometry
+    // per lane
+    int up = 0;
+    uint32_t dst = 0;
+    float fx = 0.0f, fy = 0.0f;
+    Path S;
+    Hit h;
+    bool has = false;
+    float tmax = RT_INFINITY, a = 0.0f;
+    v3 inv = mk3s(0.0f);
+    uint32_t nx = RT_LINK_END;
+    int status = RT_SM_FRESH;
+    // a bound on the wave's time (4x the chunk-wait bound): past it the wave sets the
+    // fault word (rt_sync reports it) and leaves, so a bug cannot keep the grid resident
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    uint32_t pass = 0;
+    for (;;) {
+        if ((++pass & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t_start > 4 * RT_CHUNK_WAIT_TICKS) {
+            __hip_atomic_store((gu32*)P.fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        // fold the units whose samples are all stored, oldest first (ordered / one chunk)
+        if (!staged) {
+#pragma unroll 1
+            for (int k = 0; k < 2; k++) {
+                const bool l0 = unit0 >= 0, l1 = unit1 >= 0;
+                if (!l0 && !l1) break;
+                const int p = (l0 && (!l1 || unit0 < unit1)) ? 0 : 1;
+                const UnitGeo g = unit_geo(P, p ? unit1 : unit0, n_tiles, tiles_x);
+                if ((p == cur && next < g.total) || (p ? done1 : done0) < g.total) break;
+                // all of the unit's colours are in slot p: fold them per pixel in frame order
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (g.chunk > 0) wait_chunk(P, g.tile, g.chunk);
+                if ((lane & 7) < g.wt && (lane >> 3) < g.ht) {
+                    const float4* ws = wbase + (size_t)p * slot_f4;
+                    float4* px = reinterpret_cast<float4*>(P.image) + (size_t)(g.ly0 + (lane >> 3)) * P.width +
+                                 g.tx0 + (lane & 7);
+                    float4 prev = *px;
+                    for (int f = g.f0; f < g.f1; f++) {
+                        const float4 c4 = ws[(f - g.f0) * 64 + lane];
+                        const int fcnt = P.first_frame + f;
+                        const float n1 = (float)(fcnt - 1), n = (float)fcnt;
+                        prev.x = (prev.x * n1 + c4.x) / n;
+                        prev.y = (prev.y * n1 + c4.y) / n;
+                        prev.z = (prev.z * n1 + c4.z) / n;
+                        prev.w = 1.0f;
+                    }
+                    *px = prev;
+                }
+                if (g.chunk + 1 < P.n_chunks) publish_chunk(P, g.tile, g.chunk);
+                if (p) {
+                    unit1 = -1;
+                    done1 = 0;
+                } else {
+                    unit0 = -1;
+                    done0 = 0;
+                }
+            }
+        }
+        // claim samples for the FRESH lanes (compute.glsl:345-350); a new unit when the
+        // pool's unit has none left
+        bool fin = false;   // a sample stored in this pass (max_depth 0)
+        for (;;) {
+            const unsigned long long need = __ballot(status == RT_SM_FRESH);
+            if (need == 0) break;
+            if (next >= total_cur) {
+                if (no_more) break;
+                const int o = staged ? 0 : cur ^ 1;
+                if (!staged && (o ? unit1 : unit0) >= 0) break;   // both slots in use: the FRESH lanes wait
+                int u = 0;
+                if (lane == 0) u = atomicAdd(P.tile_counter, 1);
+                u = __builtin_amdgcn_readfirstlane(__shfl(u, 0));
+                if (u >= n_units) {
+                    no_more = true;
+                    break;
+                }
+                if (!staged) {
+                    if (o) unit1 = u;
+                    else unit0 = u;
+                }
+                cur = o;
+                gc = unit_geo(P, u, n_tiles, tiles_x);
+                total_cur = gc.total;
+                next = 0;
+                continue;
+            }
+            if (status == RT_SM_FRESH) {
+                const uint32_t s = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                if (s < total_cur) {
+                    // sample s of the pool unit: frame-in-chunk, then pixel (shifts for a full tile)
+                    uint32_t fl, py, px;
+                    if (gc.wt == 8 && gc.ht == 8) {
+                        fl = s >> 6;
+                        py = (s >> 3) & 7u;
+                        px = s & 7u;
+                    } else {
+                        const uint32_t nv = (uint32_t)(gc.wt * gc.ht);
+                        fl = s / nv;
+                        const uint32_t pp = s - fl * nv;
+                        py = pp / (uint32_t)gc.wt;
+                        px = pp - py * (uint32_t)gc.wt;
+                    }
+                    const int lr = gc.ly0 + (int)py, x = gc.tx0 + (int)px;
+                    const int y = P.world == 1 ? lr
+                                               : ((lr / P.stripe_rows) * P.world + P.rank) * P.stripe_rows +
+                                                     lr % P.stripe_rows;
+                    const int f = gc.f0 + (int)fl;
+                    up = cur;
+                    dst = staged ? (uint32_t)f * (uint32_t)P.n_pixels + (uint32_t)lr * (uint32_t)P.width + (uint32_t)x
+                                 : fl * 64u + py * 8u + px;
+                    fx = (float)x;
+                    fy = (float)y;
+                    unsigned long long t0 = STATS ? clock64() : 0;
+                    if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
+                    const v3 pbase = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)),
+                                          scale3(ld3(C.pixel_delta_v), fy));
+                    start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, pbase);
+                    if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
+                    if (P.max_depth <= 0) {   // the loop never runs: final_color vec3(0)
+                        const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        if (staged) P.samples[dst] = z4;
+                        else wbase[(size_t)up * slot_f4 + dst] = z4;
+                        fin = true;
+                    } else {
+                        status = RT_SM_BEGIN;
+                    }
+                }
+            }
+            next = min(next + (uint32_t)__popcll(need), total_cur);
+            if (__ballot(fin)) break;   // count these before claiming more (below)
+        }
+        // a new walk (bounce(): depth, a zero direction hits nothing, compute.glsl:226-229)
+        if (status == RT_SM_BEGIN) {
+            S.depth++;
+            h.t = 0.0f; h.type = 0; h.idx = 0; h.face = 0;
+            h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
+            has = false;
+            tmax = RT_INFINITY;
+            nx = 0u;
+            const bool dir_zero = (S.d.x == 0.0f) && (S.d.y == 0.0f) && (S.d.z == 0.0f);
+            status = (dir_zero || P.n_nodes == 0) ? RT_SM_HIT : RT_SM_TRACE;
+            if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);
+        }
+        // per-ray constants of every walk (new or resumed: the same values again)
+        if (status == RT_SM_TRACE) {
+            inv = mk3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
+            a = g_dot(S.d, S.d);
+        }
+        // rounds of node walk + leaf tests (trace())
+        for (;;) {
+            const unsigned long long tr = __ballot(status == RT_SM_TRACE);
+            const int n_hit = __popcll(__ballot(status == RT_SM_HIT));
+            if (STATS && tr) st_pred(st, status == RT_SM_FRESH, ST_RET_IT, ST_RET_LN);
+            if (tr == 0 || n_hit >= batch || n_hit * 64 >= P.sm_frac * (n_hit + __popcll(tr))) break;
+            const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
+            const bool wave_exact = __ballot(status == RT_SM_TRACE && lane_exact) != 0;
+            if (status == RT_SM_TRACE) {
+                if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
+                unsigned long long t0 = STATS ? clock64() : 0;
+                if (P.walk_frac >= 64) {
+                    nx = wave_exact ? link_walk<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, st)
+                                    : link_walk<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, st);
+                } else {
+                    const int needw = (__popcll(__ballot(1)) * P.walk_frac + 63) >> 6;
+                    nx = wave_exact ? link_walk_part<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, needw, st)
+                                    : link_walk_part<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, needw, st);
+                }
+                if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
+                if ((int)nx >= 0) {
+                    // still walking: the next round goes on from nx
+                } else if (nx == RT_LINK_END) {
+                    status = RT_SM_HIT;
+                } else {
+                    unsigned long long t1 = STATS ? clock64() : 0;
+                    if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+                    const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
+                    leaf_prims_t<STATS, FD>(P, lf.x, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf, fx, fy, h,
+                                            has, st);
+                    if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+                    nx &= 0xFFFFu;
+                    if (nx == 0xFFFFu) status = RT_SM_HIT;
+                }
+            }
+        }
+        // shade the HIT lanes together
+        if (status == RT_SM_HIT) {
+            unsigned long long ts = STATS ? clock64() : 0;
+            if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
+            v3 cur3;
+            h.t = tmax;   // the accepted hit's t (unused on a miss)
+            bool done = after_trace(P, S, h, has, fx, fy, cur3);
+            if (!done && S.depth >= P.max_depth) {   // the loop is exhausted: final_color stays vec3(0)
+                cur3 = mk3s(0.0f);
+                done = true;
+            }
+            if (done) {
+                const float4 c4 = make_float4(cur3.x, cur3.y, cur3.z, 0.0f);
+                if (staged) P.samples[dst] = c4;
+                else wbase[(size_t)up * slot_f4 + dst] = c4;
+                fin = true;
+                status = RT_SM_FRESH;
+            } else {
+                status = RT_SM_BEGIN;
+            }
+            if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
+        }
+        // the samples stored in this pass, per slot
+        const unsigned long long f_all = __ballot(fin), f_one = __ballot(fin && up == 1);
+        done0 += (uint32_t)__popcll(f_all & ~f_one);
+        done1 += (uint32_t)__popcll(f_one);
+        // the end: no unit left to claim, every lane idle, every slot folded
+        if (no_more && __ballot(status != RT_SM_FRESH) == 0 && (staged || (unit0 < 0 && unit1 < 0))) break;
+    }
+}
+
 // Persistent kernel: one resident grid; each workgroup stages the BVH (link
 // format, 57 KB for scene 8), the Perlin table and the media records in LDS
 // once, then each wave repeatedly takes the next work unit from a device-wide
@@ -1809,7 +2088,9 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
     const int tiles_x = (P.width + 7) >> 3;
     const int n_tiles = tiles_x * ((P.local_rows + 7) >> 3);
     const int n_units = n_tiles * P.n_chunks;
-    for (;;) {
+    if (LINK && !FAST && (OPT & RT_OPT_SM) && (OPT & RT_OPT_STREAM)) {
+        render_stream<STATS, OPT, (OPT & RT_OPT_FD) != 0>(P, rnodes, (int)blockIdx.x * (BLOCK / 64) + (tid >> 6), st);
+    } else for (;;) {
         int unit = 0;
         if (lane == 0) unit = atomicAdd(P.tile_counter, 1);
         unit = __builtin_amdgcn_readfirstlane(__shfl(unit, 0));   // wave-uniform (scalar)
@@ -1949,9 +2230,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     // Variants (RT_KERNEL_VARIANT; all bit-identical, tests/test_gpu_boundary.py):
-    //   0: pooled units with walks and shading in batches (render_sm) over link-format nodes in
-    //      LDS (+ the Perlin table and media records), 512 threads, 4 waves per SIMD; 39 its stats
-    //      twin.  Falls back to pooled units over the threaded meta-word nodes (LDS, else global)
+    //   0: pooled samples streamed over units with walks and shading in batches (render_stream)
+    //      over link-format nodes in LDS (+ the Perlin table and media records), 512 threads,
+    //      4 waves per SIMD; 39 its stats twin.  Falls back to pooled units over the threaded meta-word nodes (LDS, else global)
     //      when the link format is unavailable (> 2047 nodes) or does not fit LDS.
     //   40: pooled units, one bounce at a time for the whole wave (render_pool); 41 its stats twin.
     //   37: the link walk with one pixel per lane (render_pixel); 38 its stats twin.
@@ -1967,9 +2248,12 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
                             : 0;
     const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
     const size_t lds_p = lds_t > extra_end ? lds_t : extra_end;
-    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39 || a.variant == 41;
-    const bool pool = a.variant == 0 || a.variant == 39 || a.variant == 40 || a.variant == 41;
-    const bool sm = a.variant == 0 || a.variant == 39;
+    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39 || a.variant == 41 ||
+                       a.variant == 44;
+    const bool pool = a.variant == 0 || a.variant == 39 || a.variant == 40 || a.variant == 41 || a.variant == 43 ||
+                      a.variant == 44;
+    const bool sm = a.variant == 0 || a.variant == 39 || a.variant == 43 || a.variant == 44;
+    const bool streamed = a.variant == 0 || a.variant == 39;
     if (pool && !a.samples && !a.wbuf) return -1;   // pooled ordered / one-chunk units need the per-wave slots
     const size_t acc = RT_LDS_ACC_BYTES;
     // the launch shape and its staged bytes (before the running-mean slots)
@@ -2018,7 +2302,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
         case FAST_LDS: rc = RT_LAUNCH(false, true, true, 0); break;
         case FAST_GLOBAL: rc = RT_LAUNCH(false, false, true, 0); break;
         case LINK_LDS:
-            rc = sm && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD)
+            rc = streamed && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
+                 : streamed ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM)
+                 : sm && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD)
                  : sm   ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM)
                  : pool ? RT_LAUNCH(true, true, false, RT_OPT_POOL)
                         : RT_LAUNCH(true, true, false, 0);
