@@ -17,8 +17,8 @@
 //   image    : float4 [padded_local_rows][W], stripe-compacted rows
 //   tile_done: uint32 [tiles] chunks published per 8x8 tile (ordered-chunk launches)
 //   samples  : float4 [frames][local_rows*W] per-frame colours (staged-chunk launches)
-//   wbuf     : float4 [resident waves][chunk_frames][64] per-wave sample colours of the
-//              unit in flight (pooled units, ordered / one-chunk launches)
+//   wbuf     : float4 [resident waves][2][chunk_frames][64] per-wave sample colours of the
+//              units in flight (pooled units, ordered / one-chunk launches)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -97,7 +97,7 @@ struct rt_kernel_args {
     float4* samples;             // staged chunks: per-frame colours [n_frames][n_pixels]; nullptr = ordered / one chunk
     size_t n_pixels;             // local_rows * width
     unsigned* fault;             // set when an ordered-chunk wait times out (rt_sync reports it)
-    float4* wbuf;                // pooled units, ordered / one chunk: per resident wave 64 * chunk_frames colours
+    float4* wbuf;                // pooled units, ordered / one chunk: per resident wave 2 x 64 x chunk_frames colours
     int wbuf_waves;              // waves wbuf has slots for (the launch's grid never exceeds it)
     int sm_batch;                // render_sm: shade once this many lanes' walks ended,
     int sm_frac;                 // or this many 64ths of the lanes with a walk (or none runs)

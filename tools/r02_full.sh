@@ -14,8 +14,8 @@ step pmc_c5 600 python tools/pmc_profile.py --groups 0,2,3,4 --target "--scene 8
 # the bench's roofline reads profiles/valu.json: this run's counts
 cp gpurun_out/valu.json profiles/valu.json
 step bench_c3 400 python bench.py
-step bench_c2 200 python bench.py --preset c2 --no-cpu-baseline
-step bench_c4 200 python bench.py --preset c4 --no-cpu-baseline
+step bench_c2 300 python bench.py --preset c2 --cpu-seconds 30
+step bench_c4 300 python bench.py --preset c4 --cpu-seconds 30
 step bench_c5 300 python bench.py --preset c5 --no-cpu-baseline --steps 4
 step rocprof_c3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --no-cpu-baseline
 step kstats_s8 300 python tools/kernel_stats.py --scene 8 --frames 64
