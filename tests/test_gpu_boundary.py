@@ -140,29 +140,44 @@ def test_bound_torch_image_and_stream(gpu):
 VARIANTS = [0, 43, 40, 37, 30, 61]   # streamed batched pooled samples (default), batched per unit, pooled units, one pixel per lane, threaded meta walk, exact near-first walk
 
 
+# work splits (rt_capi.hip rt_render): one unit per tile with all frames (folded per
+# wave), ordered frame chunks handed over between waves, staged chunks (the default)
+SPLITS = {
+    "direct": {"RT_CHUNK_TARGET": "0"},
+    "ordered1": {"RT_STAGE_TILES": "0", "RT_CHUNK_TARGET": "1"},
+    "ordered16": {"RT_STAGE_TILES": "0", "RT_CHUNK_TARGET": "16"},
+    "ordered_max": {"RT_STAGE_TILES": "0", "RT_CHUNK_TARGET": "100000"},
+    "staged": {},
+    "staged_max": {"RT_STAGED_CHUNK_TARGET": "100000"},
+}
+
+
 @pytest.mark.parametrize("sid", [8, 6, 7])
-@pytest.mark.parametrize("chunk_target", ["0", "1", "16", "100000"])
-def test_all_kernel_variants_identical(gpu, monkeypatch, chunk_target, sid):
+@pytest.mark.parametrize("split", list(SPLITS))
+def test_all_kernel_variants_identical(gpu, monkeypatch, split, sid):
     """Every launch shape of the kernel (RT_KERNEL_VARIANT) and every work split
-    (RT_CHUNK_TARGET: 0 = one unit per tile with all frames, else tile x ordered
-    frame-chunk units handed over between waves) renders the same bits; scenes 8
-    (canonical boxes, media, Perlin, image texture), 6 and 7 (rotated boxes: the
-    general box test)."""
+    (SPLITS) renders the same bits; scenes 8 (canonical boxes, media, Perlin, image
+    texture), 6 and 7 (rotated boxes: the general box test)."""
     s = rtamd.Scene(sid, 40, 24, seed=1)
     ref = oracle_image(s, 6)
-    monkeypatch.setenv("RT_CHUNK_TARGET", chunk_target)
+    for k, v in SPLITS[split].items():
+        monkeypatch.setenv(k, v)
     for v in VARIANTS:
         monkeypatch.setenv("RT_KERNEL_VARIANT", str(v))
         out = gpu_image(s, 6)
-        assert bit_equal(out, ref), f"variant {v}, chunk target {chunk_target}: {mismatch_report(out, ref)}"
+        assert bit_equal(out, ref), f"variant {v}, split {split}: {mismatch_report(out, ref)}"
 
 
-def test_ordered_chunk_chain_small_image(gpu, monkeypatch):
-    """Few tiles, many chunks: each of the 15 tiles' 200 one-frame chunks waits for the
-    previous one (the hand-off is on the critical path), over 2 launches (256 + 44 frames)."""
+@pytest.mark.parametrize("split", ["ordered_max", "staged_max"])
+def test_chunk_chain_small_image(gpu, monkeypatch, split):
+    """Few tiles, many chunks: each of the 15 tiles' 300 frames in one-frame chunks over
+    2 launches (150 + 150 frames): ordered, every chunk waits for the previous one (the
+    hand-off is on the critical path; render_stream folds two units per wave in claim
+    order); staged, every chunk's colours folded by fold_kernel."""
     s = rtamd.Scene(8, 40, 24, seed=1)
     ref = oracle_image(s, 300, spp=300)
-    monkeypatch.setenv("RT_CHUNK_TARGET", "100000")
+    for k, v in SPLITS[split].items():
+        monkeypatch.setenv(k, v)
     out = gpu_image(s, 300, spp=300)
     assert bit_equal(out, ref), mismatch_report(out, ref)
 

@@ -92,8 +92,14 @@ def test_full_size_stripe_partition_equals_one_gpu(gpu, world):
 @pytest.mark.parametrize("sid", [8, 0])
 def test_ordered_chunks_equal_whole_launch_1080p(gpu, monkeypatch, sid):
     """64 frames at 1080p as 64 one-frame chunks per tile (32 400 tiles, 63 wave-to-wave
-    hand-offs each, every chunk on whichever CU/XCD dequeues it) == one unit per tile."""
+    hand-offs each, every chunk on whichever CU/XCD dequeues it) == one unit per tile
+    == 64 staged one-frame chunks per tile (the default's split, at its extreme)."""
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
     whole = render(scene, 64, 5, 4096, chunk_target=0, monkeypatch=monkeypatch)
+    monkeypatch.setenv("RT_STAGE_TILES", "0")
     chunked = render(scene, 64, 5, 4096, chunk_target=100000, monkeypatch=monkeypatch)
     assert bit_equal(chunked, whole), mismatch_report(chunked, whole)
+    monkeypatch.delenv("RT_STAGE_TILES")
+    monkeypatch.setenv("RT_STAGED_CHUNK_TARGET", "100000")
+    staged = render(scene, 64, 5, 4096, chunk_target=16, monkeypatch=monkeypatch)
+    assert bit_equal(staged, whole), mismatch_report(staged, whole)
