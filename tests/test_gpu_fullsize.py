@@ -103,3 +103,15 @@ def test_ordered_chunks_equal_whole_launch_1080p(gpu, monkeypatch, sid):
     monkeypatch.setenv("RT_STAGED_CHUNK_TARGET", "100000")
     staged = render(scene, 64, 5, 4096, chunk_target=16, monkeypatch=monkeypatch)
     assert bit_equal(staged, whole), mismatch_report(staged, whole)
+
+
+@pytest.mark.parametrize("knob", ["RT_BOX_PRETEST", "RT_FASTDIV"])
+def test_exactness_shortcuts_change_no_bit_1080p(gpu, monkeypatch, knob):
+    """The box bounds pre-test and the shared-reciprocal divisions against
+    the plain tests, whole 1080p images of scene 8 (every ray of 8 frames, ground boxes
+    seen at grazing angles): the same bits."""
+    scene = rtamd.Scene(8, 1920, 1080, seed=1)
+    on = render(scene, 8, 5, 4096)
+    monkeypatch.setenv(knob, "0")
+    off = render(scene, 8, 5, 4096)
+    assert bit_equal(on, off), mismatch_report(on, off)
