@@ -123,9 +123,9 @@ struct rt_ctx {
     int stage_tiles = 1 << 20;      // in effect always staged (the measured best with render_stream)
     bool fastdiv = true;   // shared-reciprocal divisions where exact (env RT_FASTDIV=0 disables; A/B)
     bool box_pretest = true;   // the canonical box tests' bounds pre-test (env RT_BOX_PRETEST=0 disables; A/B)
-    int sm_batch = 64;   // render_sm's shading batch (env RT_SM_BATCH) ...
+    int sm_batch = 64;   // render_stream's shading batch (env RT_SM_BATCH) ...
     int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
-    int walk_frac = 48;  // render_sm: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
+    int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
     size_t sample_budget = (size_t)32 << 30;
 };
 
@@ -755,11 +755,10 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
         return fail(RT_ERR_INVALID_ARG, "rt_create: bad device count");
     rt_ctx* c = new rt_ctx();
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) {
-        // 0 (default), 43, 40, 37, 30, 61 and their stats twins 39, 44, 41, 38, 31, 69
+        // 0 (default), 37, 30, 61 and their stats twins 39, 38, 31, 69
         // (rt_kernel.hip rt_launch_render); anything else is the default
         const int want = std::atoi(v);
-        c->variant = (want == 30 || want == 31 || want == 37 || want == 38 || want == 39 || want == 40 || want == 41 ||
-                      want == 43 || want == 44 || want == 61 || want == 69)
+        c->variant = (want == 30 || want == 31 || want == 37 || want == 38 || want == 39 || want == 61 || want == 69)
                          ? want
                          : 0;
     }
@@ -1235,8 +1234,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             else if (staged) a.samples = (float4*)d.samples.ptr;
             a.wbuf = nullptr;
             a.wbuf_waves = 0;
-            if (!a.samples && (c->variant == 0 || c->variant == 39 || c->variant == 40 || c->variant == 41 ||
-                               c->variant == 43 || c->variant == 44)) {
+            if (!a.samples && (c->variant == 0 || c->variant == 39)) {
                 // pooled units fold per wave; two slots per wave (render_stream keeps two units in flight)
                 const size_t need = (size_t)waves * 2 * 64 * (size_t)a.chunk_frames * sizeof(float4);
                 if (d.wbuf.bytes < need) {
@@ -1454,8 +1452,6 @@ static int stats_twin(int v) {
     if (v == 61 || v == 69) return 69;
     if (v == 30 || v == 31) return 31;
     if (v == 37 || v == 38) return 38;
-    if (v == 40 || v == 41) return 41;
-    if (v == 43 || v == 44) return 44;
     return 39;
 }
 

@@ -38,7 +38,7 @@ typedef rt_kernel_args KP;
 
 // OPT bits of the kernel templates
 #define RT_OPT_POOL 1   // pooled units (render_pool): without it a lane owns a pixel (variant 37)
-#define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_sm)
+#define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_stream)
 #define RT_OPT_FD 4     // with RT_OPT_SM: the scene is in the shared-reciprocal division regime (P.fastdiv)
 #define RT_OPT_STREAM 8 // with RT_OPT_SM: the wave streams over units (render_stream) instead of one at a time
 
@@ -78,7 +78,7 @@ enum {
     // link walk: traces begun (wave calls, lanes), and rounds of its node-walk + leaf loop with the
     // lanes whose trace is still running (the rest wait for the wave's longest trace)
     ST_TRACE_IT, ST_TRACE_LN, ST_ROUND_IT, ST_ROUND_LN,
-    // render_sm rounds: lanes of the wave already retired (their unit has no samples left)
+    // render_stream rounds: lanes of the wave idle (no sample to claim: the tail of the launch)
     ST_RET_IT, ST_RET_LN, ST_N
 };
 __device__ __forceinline__ bool first_active_lane() {
@@ -1553,158 +1553,6 @@ __device__ __forceinline__ void render_pool(const KP& P, const float4* __restric
     }
 }
 
-// Pooled unit with the bounce split into stages (RT_OPT_SM, link-format walk):
-// every lane is FRESH (needs a sample), TRACE (its walk is running), HIT (walk
-// done, to be shaded) or RETIRED (no samples left).  The wave runs rounds of
-// node walk + leaf tests for its TRACE lanes until P.sm_batch lanes are HIT, or
-// P.sm_frac/64 of the lanes with a walk, or none is tracing, then shades the HIT lanes together; lanes whose path goes
-// on start their next walk, the others store their sample and claim the next.
-// So a lane whose walk ended early does not wait for the wave's longest walk:
-// it is shaded with the next batch while the other lanes' walks continue from
-// where they stopped (the walk position nx, ray_t.max and the hit record are
-// the lane's own, so each walk is the reference's, as in trace()).
-#define RT_SM_FRESH 0
-#define RT_SM_TRACE 1
-#define RT_SM_HIT 2
-#define RT_SM_RETIRED 3
-#define RT_SM_BEGIN 4   // a new walk: set up in the next pass
-// FD (P.fastdiv): the rounds' leaf tests use the shared-reciprocal divisions (one
-// form of the leaf code per kernel keeps the hot loop's registers).
-template <bool STATS, int OPT, bool FD>
-__device__ __forceinline__ void render_sm(const KP& P, const float4* __restrict__ nodes, int tx0, int ly0, int wt,
-                                          int ht, int f0, int kf, float4* wslot, unsigned long long* st) {
-    const uint32_t nv = (uint32_t)(wt * ht), total = nv * (uint32_t)kf;
-    const rt_camera_ubo& C = P.cam;
-    const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
-    const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
-    const int batch = P.sm_batch;
-    uint32_t next = 0;   // first unclaimed sample (the same in every lane)
-    uint32_t s = 0;
-    float fx = 0.0f, fy = 0.0f;
-    Path S;
-    Hit h;
-    bool has = false;
-    float tmax = RT_INFINITY, a = 0.0f;
-    v3 inv = mk3s(0.0f);
-    uint32_t nx = RT_LINK_END;
-    int status = RT_SM_FRESH;
-    for (;;) {
-        // claim samples for the FRESH lanes and start their paths (compute.glsl:345-350)
-        for (;;) {
-            const unsigned long long need = __ballot(status == RT_SM_FRESH);
-            if (need == 0) break;
-            if (status == RT_SM_FRESH) {
-                s = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                if (s >= total) {
-                    status = RT_SM_RETIRED;
-                } else {
-                    uint32_t fl, py, px;
-                    if (nv == 64) {   // a full tile: shifts
-                        fl = s >> 6;
-                        py = (s >> 3) & 7u;
-                        px = s & 7u;
-                    } else {
-                        fl = s / nv;
-                        const uint32_t p = s - fl * nv;
-                        py = p / (uint32_t)wt;
-                        px = p - py * (uint32_t)wt;
-                    }
-                    const int lr = ly0 + (int)py, x = tx0 + (int)px;
-                    const int y = P.world == 1 ? lr
-                                               : ((lr / P.stripe_rows) * P.world + P.rank) * P.stripe_rows +
-                                                     lr % P.stripe_rows;
-                    fx = (float)x;
-                    fy = (float)y;
-                    unsigned long long t0 = STATS ? clock64() : 0;
-                    if (STATS) st_lanes(st, ST_START_IT, ST_START_LN);
-                    const v3 pbase = add3(add3(ld3(C.up_left), scale3(ld3(C.pixel_delta_u), fx)),
-                                          scale3(ld3(C.pixel_delta_v), fy));
-                    const int f = f0 + (int)fl;
-                    start_path(P, S, P.first_frame + f, P.rand_factors[f], fx, fy, pbase);
-                    if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
-                    if (P.max_depth <= 0) store_sample(P, wslot, s, nv, wt, tx0, ly0, f0, mk3s(0.0f));
-                    else status = RT_SM_BEGIN;   // a new walk
-                }
-            }
-            next += (uint32_t)__popcll(need);
-        }
-        // a new walk (bounce(): depth, a zero direction hits nothing, compute.glsl:226-229)
-        if (status == RT_SM_BEGIN) {
-            S.depth++;
-            h.t = 0.0f; h.type = 0; h.idx = 0; h.face = 0;
-            h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
-            has = false;
-            tmax = RT_INFINITY;
-            nx = 0u;
-            const bool dir_zero = (S.d.x == 0.0f) && (S.d.y == 0.0f) && (S.d.z == 0.0f);
-            status = (dir_zero || P.n_nodes == 0) ? RT_SM_HIT : RT_SM_TRACE;
-            if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);
-        }
-        // per-ray constants of every walk (new or resumed: the same values again)
-        if (status == RT_SM_TRACE) {
-            inv = mk3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
-            a = g_dot(S.d, S.d);
-        }
-        if (__ballot(status == RT_SM_TRACE || status == RT_SM_HIT) == 0) break;   // every lane retired
-        // rounds of node walk + leaf tests (trace())
-        for (;;) {
-            const unsigned long long tr = __ballot(status == RT_SM_TRACE);
-            const int n_hit = __popcll(__ballot(status == RT_SM_HIT));
-            if (STATS && tr) st_pred(st, status == RT_SM_RETIRED, ST_RET_IT, ST_RET_LN);
-            if (tr == 0 || n_hit >= batch || n_hit * 64 >= P.sm_frac * (n_hit + __popcll(tr))) break;
-            const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
-            const bool wave_exact = __ballot(status == RT_SM_TRACE && lane_exact) != 0;
-            if (status == RT_SM_TRACE) {
-                if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
-                unsigned long long t0 = STATS ? clock64() : 0;
-                if (P.walk_frac >= 64) {
-                    nx = wave_exact ? link_walk<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, st)
-                                    : link_walk<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, st);
-                } else {
-                    const int need = (__popcll(__ballot(1)) * P.walk_frac + 63) >> 6;
-                    nx = wave_exact ? link_walk_part<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, need, st)
-                                    : link_walk_part<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, need, st);
-                }
-                if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
-                if ((int)nx >= 0) {
-                    // still walking: the next round goes on from nx
-                } else if (nx == RT_LINK_END) {
-                    status = RT_SM_HIT;
-                } else {
-                    unsigned long long t1 = STATS ? clock64() : 0;
-                    if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-                    const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
-                    leaf_prims_t<STATS, FD>(P, lf.x, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf, fx, fy, h,
-                                            has, st);
-                    if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-                    nx &= 0xFFFFu;
-                    if (nx == 0xFFFFu) status = RT_SM_HIT;
-                }
-            }
-        }
-        // shade the HIT lanes together
-        if (status == RT_SM_HIT) {
-            unsigned long long ts = STATS ? clock64() : 0;
-            if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
-            v3 cur;
-            h.t = tmax;   // the accepted hit's t (unused on a miss)
-            bool done = after_trace(P, S, h, has, fx, fy, cur);
-            if (!done && S.depth >= P.max_depth) {   // the loop is exhausted: final_color stays vec3(0)
-                cur = mk3s(0.0f);
-                done = true;
-            }
-            if (done) {
-                store_sample(P, wslot, s, nv, wt, tx0, ly0, f0, cur);
-                status = RT_SM_FRESH;
-            } else {
-                status = RT_SM_BEGIN;
-            }
-            if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
-        }
-    }
-}
-
 // Ordered chunks (a launch over few tiles per resident wave, e.g. the stripe set
 // of one of N GPUs): the work unit is one 8x8 tile x one chunk of the launch's
 // frames, unit = chunk * n_tiles + tile, so chunk k of a tile is dequeued after
@@ -1744,7 +1592,25 @@ __device__ __forceinline__ void publish_chunk(const KP& P, int tile, int chunk) 
     __hip_atomic_store((gu32*)(P.tile_done + tile), (unsigned)(chunk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// render_sm over a stream of units (RT_OPT_STREAM): when the wave's current unit
+// Walks and shading in batches (RT_OPT_SM, link-format walk): every lane is
+// FRESH (needs a sample), TRACE (its walk is running), HIT (walk done, to be
+// shaded) or BEGIN (a new walk, set up in the next pass).  The wave runs rounds
+// of node walk + leaf tests for its TRACE lanes until P.sm_batch lanes are HIT,
+// or P.sm_frac/64 of the lanes with a walk, or none is tracing, then shades the
+// HIT lanes together; lanes whose path goes on start their next walk, the others
+// store their sample and claim the next.  So a lane whose walk ended early does
+// not wait for the wave's longest walk: it is shaded with the next batch while
+// the other lanes' walks continue from where they stopped (the walk position nx,
+// ray_t.max and the hit record are the lane's own, so each walk is the
+// reference's, as in trace()).  FD (P.fastdiv): the rounds' leaf tests use the
+// shared-reciprocal divisions (one form of the leaf code per kernel keeps the hot
+// loop's registers).
+#define RT_SM_FRESH 0
+#define RT_SM_TRACE 1
+#define RT_SM_HIT 2
+#define RT_SM_BEGIN 4
+//
+// The batched walks over a stream of units (RT_OPT_STREAM): when the wave's current unit
 // has no unclaimed samples left, the wave claims its next unit and its free lanes
 // take that unit's samples while the other lanes finish the previous unit's paths
 // (before, they idled through the unit's tail: 8.5% of lane-rounds on scene 8).
@@ -2106,12 +1972,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             const int tx0 = x - (lane & 7), ly0 = lr - (lane >> 3);
             float4* wslot =
                 ordered ? P.wbuf + ((size_t)blockIdx.x * (BLOCK / 64) + (tid >> 6)) * 64 * P.chunk_frames : nullptr;
-            if (LINK && !FAST && (OPT & RT_OPT_SM))
-                render_sm<STATS, OPT, (OPT & RT_OPT_FD) != 0>(P, rnodes, tx0, ly0, min(8, P.width - tx0),
-                                                              min(8, P.local_rows - ly0), f0, f1 - f0, wslot, st);
-            else
-                render_pool<LINK, STATS, FAST, OPT>(P, rnodes, fc, tx0, ly0, min(8, P.width - tx0),
-                                                    min(8, P.local_rows - ly0), f0, f1 - f0, wslot, st);
+            render_pool<LINK, STATS, FAST, OPT>(P, rnodes, fc, tx0, ly0, min(8, P.width - tx0),
+                                                min(8, P.local_rows - ly0), f0, f1 - f0, wslot, st);
             if (!ordered) continue;
             // the unit's colours, written by any lane of this wave, folded by the pixel's lane
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2232,13 +2094,15 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     // Variants (RT_KERNEL_VARIANT; all bit-identical, tests/test_gpu_boundary.py):
     //   0: pooled samples streamed over units with walks and shading in batches (render_stream)
     //      over link-format nodes in LDS (+ the Perlin table and media records), 512 threads,
-    //      4 waves per SIMD; 39 its stats twin.  Falls back to pooled units over the threaded meta-word nodes (LDS, else global)
-    //      when the link format is unavailable (> 2047 nodes) or does not fit LDS.
-    //   40: pooled units, one bounce at a time for the whole wave (render_pool); 41 its stats twin.
-    //   37: the link walk with one pixel per lane (render_pixel); 38 its stats twin.
+    //      4 waves per SIMD; 39 its stats twin.  Falls back to pooled units one bounce at a
+    //      time (render_pool) over the threaded meta-word nodes (LDS, else global) when the
+    //      link format is unavailable (> 2047 nodes) or does not fit LDS.
+    //   37: the link walk with one pixel per lane (render_pixel, the round-1 default); 38 its
+    //      stats twin.
     //   30: threaded nodes with the meta word (in LDS when they fit, else global); 31 stats twin.
     //   61: the exact near-first stack walk (tree and stacks in LDS); 69 stats twin.
-    // Every shape's dynamic LDS ends with the lanes' running-mean slots (RT_LDS_ACC_BYTES).
+    // Every shape's dynamic LDS ends with the lanes' running-mean slots (RT_LDS_ACC_BYTES;
+    // used by the one-pixel-per-lane kernels).
     const size_t lds_t = (size_t)a.n_nodes * sizeof(rt_dnode);   // threaded nodes
     const bool fits_t = lds_t <= RT_LDS_NODE_BYTES;
     // after the nodes, as placed by the host: the Perlin table, then the media records
@@ -2248,12 +2112,8 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
                             : 0;
     const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
     const size_t lds_p = lds_t > extra_end ? lds_t : extra_end;
-    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39 || a.variant == 41 ||
-                       a.variant == 44;
-    const bool pool = a.variant == 0 || a.variant == 39 || a.variant == 40 || a.variant == 41 || a.variant == 43 ||
-                      a.variant == 44;
-    const bool sm = a.variant == 0 || a.variant == 39 || a.variant == 43 || a.variant == 44;
-    const bool streamed = a.variant == 0 || a.variant == 39;
+    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39;
+    const bool pool = a.variant == 0 || a.variant == 39;   // the default and its stats twin
     if (pool && !a.samples && !a.wbuf) return -1;   // pooled ordered / one-chunk units need the per-wave slots
     const size_t acc = RT_LDS_ACC_BYTES;
     // the launch shape and its staged bytes (before the running-mean slots)
@@ -2302,12 +2162,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
         case FAST_LDS: rc = RT_LAUNCH(false, true, true, 0); break;
         case FAST_GLOBAL: rc = RT_LAUNCH(false, false, true, 0); break;
         case LINK_LDS:
-            rc = streamed && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
-                 : streamed ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM)
-                 : sm && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD)
-                 : sm   ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM)
-                 : pool ? RT_LAUNCH(true, true, false, RT_OPT_POOL)
-                        : RT_LAUNCH(true, true, false, 0);
+            rc = pool && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
+                 : pool            ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM)
+                                   : RT_LAUNCH(true, true, false, 0);
             break;
         case META_LDS:
             rc = pool ? RT_LAUNCH(false, true, false, RT_OPT_POOL) : RT_LAUNCH(false, true, false, 0);

@@ -137,7 +137,7 @@ def test_bound_torch_image_and_stream(gpu):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
-VARIANTS = [0, 43, 40, 37, 30, 61]   # streamed batched pooled samples (default), batched per unit, pooled units, one pixel per lane, threaded meta walk, exact near-first walk
+VARIANTS = [0, 37, 30, 61]   # streamed batched pooled samples (default), one pixel per lane (round-1 default), threaded meta walk, exact near-first walk
 
 
 # work splits (rt_capi.hip rt_render): one unit per tile with all frames (folded per
