@@ -191,16 +191,21 @@ def roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms):
         except (OSError, ValueError):
             return {}
     key = config_key(args, frames_per_launch)
-    rec = load("valu.json").get(key)
+    profiles = load("valu.json")
+    rec = profiles.get(key)
+    if not rec:   # N > 1 launches more frames of 1/N of the rows: the 64-frame profile, per sample
+        key = config_key(args, 64)
+        rec = profiles.get(key)
     if not rec:
         log(f"no committed VALU profile for {key} (profiles/valu.json); roofline omitted")
         return None
-    # the committed count is for rec["samples_per_launch"]; scale per sample if the launch differs
-    insts = rec["SQ_INSTS_VALU"] * samples_per_launch / rec["samples_per_launch"]
+    # the committed counts are for rec["samples_per_launch"]; scaled per sample if the launch differs
+    per = samples_per_launch / rec["samples_per_launch"]
+    insts = rec["SQ_INSTS_VALU"] * per
     t = avg_launch_ms * 1e-3
     achieved = insts / t / 1e9
     peak_meas = load("r02_valu_peak.json").get("wave_inst_per_s_4waves")
-    traffic = rec.get("hbm_bytes_per_launch")
+    traffic = rec["hbm_bytes_per_launch"] * per if rec.get("hbm_bytes_per_launch") else None
     lane = rec.get("valu_lane_utilization")
     out = {"bound": "valu", "achieved": round(achieved, 1), "peak": VALU_PEAK, "unit": "Gwave-inst/s",
            "frac": round(achieved / VALU_PEAK, 4), "traffic": traffic,
@@ -212,7 +217,7 @@ def roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms):
            "frac_of_measured_4wave_peak": round(achieved * 1e9 / peak_meas, 4) if peak_meas else None,
            "dram_gbs": round(traffic / t / 1e9, 1) if traffic else None,
            "dram_frac": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
-           "profile": rec.get("source"),
+           "profile": key,
            "note": "achieved = SQ_INSTS_VALU per launch (rocprofv3 PMC, profiles/valu.json) / launch time measured "
                    "live with HIP events; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction; "
                    "lane_weighted_frac counts only the active lanes; traffic = DRAM bytes per launch "
