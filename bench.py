@@ -283,7 +283,7 @@ def main():
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
-    launches_per_step = math.ceil(F / 256)
+    launches_per_step = math.ceil(F / 512)   # rt_render: equal launches of at most 512 frames
     avg_launch_ms = float(np.mean(kernel_ms)) / launches_per_step
     t_max = elapsed
     rank_ms = [avg_launch_ms]
@@ -325,7 +325,7 @@ def main():
         except Exception as e:  # the baseline is reported, not required
             log("cpu baseline failed:", repr(e))
 
-    frames_per_launch = min(F, 256)
+    frames_per_launch = math.ceil(F / launches_per_step)
     samples_per_launch = n_local_px * frames_per_launch
     roof = roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms)
 

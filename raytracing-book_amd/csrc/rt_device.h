@@ -26,7 +26,7 @@
 
 #include "rt/rt_types.h"
 
-#define RT_MAX_FRAMES_PER_LAUNCH 256
+#define RT_MAX_FRAMES_PER_LAUNCH 512
 #define RT_NODE_END 0xFFFFu
 #define RT_DFACE_F4 3    // float4 per dquads record
 #define RT_DBOX_F4 23    // float4 per dboxes record

@@ -3,7 +3,7 @@
 All through the C ABI on cuda:0, each compared bit for bit (NaN positions
 equal) against the committed golden fixtures or the CPU oracle:
 golden vectors, stripe partitions (one process per rank, several contexts on
-one GPU), ragged/tiny sizes, max_depth edge values, >256 frames per call,
+one GPU), ragged/tiny sizes, max_depth edge values, >512 frames per call,
 image write/read and resume, caller-bound device image + caller stream, every
 kernel variant, the multi-device host gather, the RaytraceExecutor mirror, and
 the ABI's error behaviour.
@@ -86,10 +86,11 @@ def test_max_depth_edges(gpu, depth):
 
 
 def test_more_frames_than_one_launch(gpu):
-    """300 frames in one rt_render call (> RT_MAX_FRAMES_PER_LAUNCH = 256)."""
+    """1100 frames in one rt_render call (> RT_MAX_FRAMES_PER_LAUNCH = 512): three equal
+    launches of 367 / 367 / 366 frames."""
     s = rtamd.Scene(3, 8, 8, seed=1)
-    ref = oracle_image(s, 300, spp=300)
-    out = gpu_image(s, 300, spp=300)
+    ref = oracle_image(s, 1100, spp=1100)
+    out = gpu_image(s, 1100, spp=1100)
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
@@ -170,15 +171,15 @@ def test_all_kernel_variants_identical(gpu, monkeypatch, split, sid):
 
 @pytest.mark.parametrize("split", ["ordered_max", "staged_max"])
 def test_chunk_chain_small_image(gpu, monkeypatch, split):
-    """Few tiles, many chunks: each of the 15 tiles' 300 frames in one-frame chunks over
-    2 launches (150 + 150 frames): ordered, every chunk waits for the previous one (the
+    """Few tiles, many chunks: each of the 15 tiles' 600 frames in one-frame chunks over
+    2 launches (300 + 300 frames): ordered, every chunk waits for the previous one (the
     hand-off is on the critical path; render_stream folds two units per wave in claim
     order); staged, every chunk's colours folded by fold_kernel."""
     s = rtamd.Scene(8, 40, 24, seed=1)
-    ref = oracle_image(s, 300, spp=300)
+    ref = oracle_image(s, 600, spp=600)
     for k, v in SPLITS[split].items():
         monkeypatch.setenv(k, v)
-    out = gpu_image(s, 300, spp=300)
+    out = gpu_image(s, 600, spp=600)
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
