@@ -102,7 +102,7 @@ struct rt_ctx {
     bool boxes_canon = false;   // every box has Box.java's axis-aligned face layout (dboxes[18..20])
     bool fd_ok[6] = {true, true, true, true, true, true};   // per binding: records in the fast-division regime
     bool fd_cam = true;
-    bool boxes_axis = false;   // every box face's u and v lie along one axis each (box pre-test)
+    bool boxes_cond = false;   // every box face's 2-D Cramer system is well conditioned (box pre-test)
     float scene_extent = -1.0f;   // max |coordinate| over records and camera (< 0: not computed)
     bool validated = false;
     uint64_t last_ns = 0;
@@ -860,17 +860,27 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
             // per box: the 6 planes first, then the 6 (A, B) pairs, then the canonical
             // planes (RT_DBOX_F4 float4)
             c->boxes_canon = true;
-            c->boxes_axis = true;
+            c->boxes_cond = true;
             for (size_t bx = 0; bx < nq / 6; bx++) {
                 float4* o = &faces[bx * RT_DBOX_F4];
                 float sw[12];
                 double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
                 for (int i = 0; i < 6; i++) {   // the bounds: every face's corners
                     const rt_quad& Q = qs[bx * 6 + i];
-                    int nz_u = 0, nz_v = 0;
+                    // the face test solves alpha, beta on the reference's axis pair (face_record);
+                    // |delta| >= half of |u_a v_b| + |u_b v_a| bounds how far a point it accepts
+                    // can lie outside the face (a few ulps of the scene's extent)
+                    {
+                        const float* u = Q.u;
+                        const float* v = Q.v;
+                        int ka = 1, kb = 2;
+                        if (u[0] * v[1] - u[1] * v[0] != 0.0f) { ka = 0; kb = 1; }
+                        else if (u[0] * v[2] - u[2] * v[0] != 0.0f) { ka = 0; kb = 2; }
+                        const double t1 = (double)u[ka] * v[kb], t2 = (double)u[kb] * v[ka];
+                        if (!(std::fabs(t1 - t2) >= 0.5 * (std::fabs(t1) + std::fabs(t2))) || t1 == t2)
+                            c->boxes_cond = false;
+                    }
                     for (int k = 0; k < 3; k++) {
-                        nz_u += Q.u[k] != 0.0f;
-                        nz_v += Q.v[k] != 0.0f;
                         for (int cu = 0; cu < 2; cu++)
                             for (int cv = 0; cv < 2; cv++) {
                                 const double x = (double)Q.q[k] + cu * (double)Q.u[k] + cv * (double)Q.v[k];
@@ -878,7 +888,6 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
                                 hi[k] = std::max(hi[k], x);
                             }
                     }
-                    if (nz_u != 1 || nz_v != 1) c->boxes_axis = false;
                 }
                 o[21] = make_float4((float)lo[0], (float)hi[0], (float)lo[1], (float)hi[1]);
                 o[22] = make_float4((float)lo[2], (float)hi[2], 0.0f, 0.0f);
@@ -1075,12 +1084,12 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.uv_always = c->uv_always;
     a.boxes_canon = c->boxes_canon ? 1 : 0;
     // Box pre-test (rt_kernel.hip leaf_prims_t): a face the exact test accepts lies, with
-    // the ray's point at its t, within ~2^-20 of the scene's extent of the box (the face
-    // tests' rounding); the kernel's slab test of the box grown by 2^-13 of that extent
-    // cannot miss it.  Needs axis-aligned faces (the face test then measures the point
-    // along the box's own axes).
+    // the ray's point at its t, within ~2^-20 of the scene's extent of the box's bounds
+    // (the face tests' rounding, amplified at most 2x by a well-conditioned 2-D solve:
+    // boxes_cond); the kernel's slab test of the bounds grown by 2^-13 of that extent
+    // cannot miss it.
     if (c->scene_extent < 0.0f) c->scene_extent = scene_extent(c);
-    a.box_margin = (c->boxes_canon && c->boxes_axis && c->box_pretest && c->scene_extent <= 0x1p60f)
+    a.box_margin = (c->boxes_cond && c->box_pretest && c->scene_extent <= 0x1p60f)
                        ? std::max(c->scene_extent, 1.0f) * 0x1p-13f
                        : 0.0f;
     a.fastdiv = (c->fastdiv && c->fd_cam && c->fd_ok[RT_BIND_SPHERES] && c->fd_ok[RT_BIND_QUADS] &&

@@ -107,7 +107,7 @@ struct rt_kernel_args {
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
     int fastdiv;                 // the scene's records are in the shared-reciprocal division regime
-    float box_margin;            // > 0: canonical box tests start with a slab test of the box's bounds
+    float box_margin;            // > 0: box tests start with a slab test of the box's bounds
                                  // grown by this margin (2^-13 of the scene's extent), which no face
                                  // the exact test accepts can lie outside; 0: no pre-test
     int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1

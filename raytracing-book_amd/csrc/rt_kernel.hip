@@ -512,7 +512,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
         } else if (ty == RT_MODEL_BOX) {
             const float4* rec = P.dboxes + RT_DBOX_F4 * ix;
             bool maybe = true;
-            if (P.box_margin > 0.0f && P.boxes_canon && fin) {
+            if (P.box_margin > 0.0f && fin) {
                 // the box's bounds grown by box_margin (rt_device.h): a ray that misses them
                 // misses every face the exact test below would accept
                 const float m = P.box_margin;

@@ -105,12 +105,13 @@ def test_ordered_chunks_equal_whole_launch_1080p(gpu, monkeypatch, sid):
     assert bit_equal(staged, whole), mismatch_report(staged, whole)
 
 
+@pytest.mark.parametrize("sid", [8, 6, 7])
 @pytest.mark.parametrize("knob", ["RT_BOX_PRETEST", "RT_FASTDIV"])
-def test_exactness_shortcuts_change_no_bit_1080p(gpu, monkeypatch, knob):
+def test_exactness_shortcuts_change_no_bit_1080p(gpu, monkeypatch, knob, sid):
     """The box bounds pre-test and the shared-reciprocal divisions against
-    the plain tests, whole 1080p images of scene 8 (every ray of 8 frames, ground boxes
-    seen at grazing angles): the same bits."""
-    scene = rtamd.Scene(8, 1920, 1080, seed=1)
+    the plain tests, whole 1080p images (every ray of 8 frames): scene 8 (ground boxes
+    seen at grazing angles), 6 and 7 (rotated boxes): the same bits."""
+    scene = rtamd.Scene(sid, 1920, 1080, seed=1)
     on = render(scene, 8, 5, 4096)
     monkeypatch.setenv(knob, "0")
     off = render(scene, 8, 5, 4096)
