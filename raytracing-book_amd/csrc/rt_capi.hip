@@ -126,6 +126,7 @@ struct rt_ctx {
     int sm_batch = 64;   // render_stream's shading batch (env RT_SM_BATCH) ...
     int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
+    bool leaf_compact = false;   // render_stream: solid leaf tests compacted across the wave (env RT_LEAF_COMPACT)
     size_t sample_budget = (size_t)32 << 30;
 };
 
@@ -770,6 +771,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_SM_BATCH")) c->sm_batch = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SM_FRAC")) c->sm_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_WALK_FRAC")) c->walk_frac = std::max(1, std::min(64, std::atoi(v)));
+    if (const char* v = std::getenv("RT_LEAF_COMPACT")) c->leaf_compact = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
@@ -1100,6 +1102,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.sm_batch = c->sm_batch;
     a.sm_frac = c->sm_frac;
     a.walk_frac = c->walk_frac;
+    a.leaf_compact = c->leaf_compact ? 1 : 0;
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);

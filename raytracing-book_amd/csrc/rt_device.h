@@ -103,6 +103,7 @@ struct rt_kernel_args {
     int sm_frac;                 // or this many 64ths of the lanes with a walk (or none runs)
     int walk_frac;               // render_sm: a round's node walk stops once this many 64ths of its lanes
                                  // hold a leaf or ended (64: all of them)
+    int leaf_compact;            // render_stream: a round's solid leaf tests compacted across the wave
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)

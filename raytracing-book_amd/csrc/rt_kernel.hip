@@ -41,6 +41,7 @@ typedef rt_kernel_args KP;
 #define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_stream)
 #define RT_OPT_FD 4     // with RT_OPT_SM: the scene is in the shared-reciprocal division regime (P.fastdiv)
 #define RT_OPT_STREAM 8 // with RT_OPT_SM: the wave streams over units (render_stream) instead of one at a time
+#define RT_OPT_COMPACT 16 // with RT_OPT_STREAM: a round's solid leaf tests compacted across the wave (leaf_round_compact)
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -60,6 +61,7 @@ __device__ __forceinline__ float4 ldg(const float4* p) {
     const f4v v = *(const g_f4v*)p;
     return make_float4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ int ldg_i(const int* p) { return *(__attribute__((address_space(1))) const int*)p; }
 
 // ---- diagnostic statistics (stats variants only; never in a timed build) ----
 // Wave-level: the first active lane adds into the wave's LDS counters, so a
@@ -161,9 +163,8 @@ __device__ __forceinline__ float div_nr(float num, float den, float r) {
 // ------------------------------------------------------------- primitives
 // hitting.glsl:17-38 — the root only.  fd: the roots as div_nr with ra =
 // rcp_nr(a), unless a lane's a = dot(dir, dir) is below 2^-60.
-__device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
-                                         float tmax, float& t, bool fd = false, float ra = 0.0f) {
-    float4 A = ldg(sp), B = ldg(sp + 1);
+__device__ __forceinline__ bool sphere_t_ab(float4 A, float4 B, float time, v3 o, v3 d, float a, float tmin,
+                                            float tmax, float& t, bool fd = false, float ra = 0.0f) {
     v3 center = add3(f3(A), scale3(f3(B), time));
     v3 oc = sub3(o, center);
     float half_b = g_dot(oc, d);
@@ -179,6 +180,10 @@ __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float ti
     }
     t = root;
     return true;
+}
+__device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
+                                         float tmax, float& t, bool fd = false, float ra = 0.0f) {
+    return sphere_t_ab(ldg(sp), ldg(sp + 1), time, o, d, a, tmin, tmax, t, fd, ra);
 }
 
 // hitting.glsl:103-124 on an intersection-only face record (rt_device.h):
@@ -210,18 +215,24 @@ __device__ __forceinline__ bool face_interior(float4 A, float4 B, v3 o, v3 d, fl
 }
 
 // hitting.glsl:90-133 without the record writes; f = dquads record.
-__device__ __forceinline__ bool quad_test(const float4* __restrict__ f, v3 o, v3 d, float tmin, float tmax, float& t,
-                                          float& alpha, float& beta, bool fd = false) {
-    float4 Q0 = ldg(f);
+// Q0, Q1 = the record's first two float4 (loaded by the caller).
+__device__ __forceinline__ bool quad_test_ab(const float4* __restrict__ f, float4 Q0, float4 Q1, v3 o, v3 d,
+                                             float tmin, float tmax, float& t, float& alpha, float& beta,
+                                             bool fd = false) {
+    const float4 Q2 = ldg(f + 2);
     v3 n = f3(Q0);
     float denom = g_dot(n, d);
     if (fabsf(denom) < 1e-8f) return false;
     const float num = Q0.w - g_dot(n, o);
     float tt = fd ? div_nr(num, denom, rcp_nr(denom)) : num / denom;
     if (!(tmin <= tt && tt <= tmax)) return false;
-    if (!face_interior(ldg(f + 1), ldg(f + 2), o, d, tt, alpha, beta, fd)) return false;
+    if (!face_interior(Q1, Q2, o, d, tt, alpha, beta, fd)) return false;
     t = tt;
     return true;
+}
+__device__ __forceinline__ bool quad_test(const float4* __restrict__ f, v3 o, v3 d, float tmin, float tmax, float& t,
+                                          float& alpha, float& beta, bool fd = false) {
+    return quad_test_ab(f, ldg(f), ldg(f + 1), o, d, tmin, tmax, t, alpha, beta, fd);
 }
 
 // hitting.glsl:135-146; fb = dboxes record.  The six faces' plane parameters
@@ -537,6 +548,147 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
     }
 }
 
+// Lanes of this wave whose bit in m is set below this lane (v_mbcnt).
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ float pull(float v, int addr) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+}
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
+
+// One round's leaf tests (compute.glsl:247-256) with the solid prims' tests
+// compacted across the wave (RT_OPT_COMPACT; called with every lane of the wave
+// active).  leaf_prims_t runs each prim type's code once per slot whenever any
+// lane has that type there: per round, box code ran 1.68 times at 17 of 64 lanes
+// and sphere code 1.19 times at 10 (profiles/r02_region_stats_s8.log).  Here the
+// round's sphere / quad / box tests of both slots form one list (boxes, spheres,
+// quads; per type slot 0 then slot 1), and lane k of the wave runs test k on its
+// owner's ray (ds_bpermute), so each type's code runs once per 64 tests.
+// Exact: a solid's result does not depend on the order of the leaf's tests except
+// through ray_t.max, and a test run with the round's ray_t.max gives the sequential
+// test's result under any smaller max m' iff its t passes m' (sphere: t < m'; the
+// larger root is >= the smaller one, so a root that fails m' leaves none; box: the
+// accepted face is the last one with the least t among the faces in range, which
+// stays the accepted one while its t <= m'; quad: one face).  So each lane applies
+// its slots in order: a solid's result against its running max, a medium's test
+// (rand() draws depend on the running max) in the lane itself, as the reference.
+// The wave's 1 KB of the lanes' running-mean LDS slots (unused by render_stream)
+// carries the test list and the results.
+template <bool STATS, bool FD>
+__device__ __forceinline__ void leaf_round_compact(const KP& P, bool at_leaf, uint32_t meta, uint32_t prims, v3 o,
+                                                   v3 d, v3 inv, float a, float time, float& tmax, float& rf,
+                                                   float px, float py, Hit& h, bool& has, float4* slots,
+                                                   unsigned long long* st) {
+    constexpr bool fd = FD;
+    const int lane = (int)__lane_id();
+    const int ty0 = at_leaf ? (int)((meta >> 16) & 0xFu) : 0;
+    const int ty1 = at_leaf ? (int)((meta >> 20) & 0xFu) : 0;
+    const int ix0 = (int)(prims & 0xFFFFu), ix1 = (int)(prims >> 16);
+    const unsigned long long b0 = __ballot(ty0 == RT_MODEL_BOX), b1 = __ballot(ty1 == RT_MODEL_BOX);
+    const unsigned long long s0 = __ballot(ty0 == RT_MODEL_SPHERE), s1 = __ballot(ty1 == RT_MODEL_SPHERE);
+    const unsigned long long q0 = __ballot(ty0 == RT_MODEL_QUAD), q1 = __ballot(ty1 == RT_MODEL_QUAD);
+    const int nb0 = __popcll(b0), nb = nb0 + __popcll(b1);
+    const int ns0 = __popcll(s0), ns = ns0 + __popcll(s1);
+    const int nq0 = __popcll(q0), n = nb + ns + nq0 + __popcll(q1);
+    int pos0 = -1, pos1 = -1;
+    if (ty0 == RT_MODEL_BOX) pos0 = lanes_below(b0);
+    else if (ty0 == RT_MODEL_SPHERE) pos0 = nb + lanes_below(s0);
+    else if (ty0 == RT_MODEL_QUAD) pos0 = nb + ns + lanes_below(q0);
+    if (ty1 == RT_MODEL_BOX) pos1 = nb0 + lanes_below(b1);
+    else if (ty1 == RT_MODEL_SPHERE) pos1 = nb + ns0 + lanes_below(s1);
+    else if (ty1 == RT_MODEL_QUAD) pos1 = nb + ns + nq0 + lanes_below(q1);
+    float4 r0 = make_float4(-1.0f, 0.0f, 0.0f, 0.0f), r1 = r0;
+    int* const sw = reinterpret_cast<int*>(slots);
+    for (int p = 0; p < n; p += 64) {   // wave-uniform; one pass unless the round has > 64 tests
+        // owners post their tests: prim index | type << 16 | owner lane << 20
+        if ((unsigned)(pos0 - p) < 64u) sw[4 * (pos0 - p) + 3] = ix0 | (ty0 << 16) | (lane << 20);
+        if ((unsigned)(pos1 - p) < 64u) sw[4 * (pos1 - p) + 3] = ix1 | (ty1 << 16) | (lane << 20);
+        wave_lds_fence();
+        const bool ex = lane < n - p;
+        int dsc = lane << 20;
+        if (ex) dsc = sw[4 * lane + 3];
+        // the owner's ray, pulled with every lane active (ds_bpermute reads active lanes only)
+        const int src = ((dsc >> 20) & 63) << 2;
+        const v3 eo = mk3(pull(o.x, src), pull(o.y, src), pull(o.z, src));
+        const v3 ed = mk3(pull(d.x, src), pull(d.y, src), pull(d.z, src));
+        const v3 ei = mk3(pull(inv.x, src), pull(inv.y, src), pull(inv.z, src));
+        const float etmax = pull(tmax, src), ea = pull(a, src), etime = pull(time, src);
+        if (ex) {
+            const int ety = (dsc >> 16) & 0xF, eix = dsc & 0xFFFF;
+            float t = 0.0f, al = 0.0f, be = 0.0f;
+            int face = 0;
+            bool hit = false;
+            if (STATS) {
+                st_pred(st, ety == RT_MODEL_SPHERE, ST_SPH_IT, ST_SPH_LN);
+                st_pred(st, ety == RT_MODEL_QUAD, ST_QUAD_IT, ST_QUAD_LN);
+                st_pred(st, ety == RT_MODEL_BOX, ST_BOX_IT, ST_BOX_LN);
+            }
+            unsigned long long c0 = STATS ? clock64() : 0;
+            if (ety == RT_MODEL_BOX) {
+                const bool fin = fabsf(eo.x) < INFINITY && fabsf(eo.y) < INFINITY && fabsf(eo.z) < INFINITY &&
+                                 fabsf(ed.x) < INFINITY && fabsf(ed.y) < INFINITY && fabsf(ed.z) < INFINITY;
+                const float4* rec = P.dboxes + RT_DBOX_F4 * eix;
+                bool maybe = true;
+                if (P.box_margin > 0.0f && fin) {   // leaf_prims_t's bounds pre-test
+                    const float m = P.box_margin;
+                    const float4 bb0 = ldg(rec + 21), bb1 = ldg(rec + 22);
+                    maybe = aabb_pk(make_float4(bb0.x - m, bb0.y + m, bb0.z - m, bb0.w + m),
+                                    make_float4(bb1.x - m, bb1.y + m, 0.0f, 0.0f), eo, ei, 0.001f, etmax);
+                }
+                if (maybe)
+                    hit = (P.boxes_canon && fin)
+                              ? box_test_canon(rec + 18, rec, eo, ed, 0.001f, etmax, t, face, al, be, fd)
+                              : box_test(rec, eo, ed, 0.001f, etmax, t, face, al, be, fd);
+                if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
+            } else if (ety == RT_MODEL_SPHERE) {
+                hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + eix), etime, eo, ed, ea, 0.001f, etmax, t,
+                               fd, fd ? rcp_nr(ea) : 0.0f);
+                if (STATS) st_add(st, ST_SPH_CYC, clock64() - c0);
+            } else {
+                hit = quad_test(P.dquads + RT_DFACE_F4 * eix, eo, ed, 0.001f, etmax, t, al, be, fd);
+                if (STATS) st_add(st, ST_QUAD_CYC, clock64() - c0);
+            }
+            slots[lane] = make_float4(hit ? t : -1.0f, al, be, __int_as_float(face));
+        }
+        wave_lds_fence();
+        if ((unsigned)(pos0 - p) < 64u) r0 = slots[pos0 - p];
+        if ((unsigned)(pos1 - p) < 64u) r1 = slots[pos1 - p];
+        wave_lds_fence();
+    }
+    // each lane's slots in order against its running ray_t.max
+#pragma unroll 1
+    for (int s = 0; s < 2; s++) {
+        const int ty = s ? ty1 : ty0, ix = s ? ix1 : ix0;
+        const float4 r = s ? r1 : r0;
+        float t = r.x;
+        bool hit;
+        if (STATS) st_pred(st, ty == RT_MODEL_CONSTANT_MEDIUM, ST_MED_IT, ST_MED_LN);
+        if (ty == RT_MODEL_CONSTANT_MEDIUM) {
+            unsigned long long c0 = STATS ? clock64() : 0;
+            hit = medium_test(P, ix, o, d, a, time, 0.001f, tmax, rf, px, py, t);
+            if (STATS) st_add(st, ST_MED_CYC, clock64() - c0);
+        } else {
+            hit = t >= 0.0f && (ty == RT_MODEL_SPHERE ? t < tmax : t <= tmax);   // t = -1: no hit (or no test)
+        }
+        if (hit) {
+            has = true;
+            tmax = t;
+            h.t = t; h.type = ty; h.idx = ix; h.face = __float_as_int(r.w);
+            if (ty == RT_MODEL_SPHERE) {
+                h.uv_kind_idx = (1 << 16) | ix;
+                h.uv_a = t;
+            } else if (ty != RT_MODEL_CONSTANT_MEDIUM) {
+                h.uv_kind_idx = 2 << 16;
+                h.uv_a = r.y;
+                h.uv_b = r.z;
+            } else {
+                h.face = 0;
+            }
+        }
+    }
+}
+
 
 // The link-format node loop from byte offset nx until a hit leaf or the end of
 // the walk (sign bit).  EXACT: the reference's per-axis slab (a -inf in 1/dir);
@@ -790,7 +942,7 @@ __device__ __forceinline__ v2 resolve_uv(const KP& P, const UvSrc& s, float time
     if (kind == 2) { v2 r = {s.a, s.b}; return r; }
     if (kind == 1) {
         const float4* sp = reinterpret_cast<const float4*>(P.spheres + (s.kind_idx & 0xFFFF));
-        float4 A = sp[0], B = sp[1];
+        float4 A = ldg(sp), B = ldg(sp + 1);
         v3 center = add3(f3(A), scale3(f3(B), time));
         return sphere_uv(sub3(mk3(s.a, s.b, s.c), center));
     }
@@ -888,7 +1040,7 @@ __device__ __forceinline__ float sphere_light_pdf(const KP& P, int idx, v3 o, v3
     const float4* sp = reinterpret_cast<const float4*>(P.spheres + idx);
     float t;
     if (!sphere_t(sp, time, o, d, g_dot(d, d), 0.001f, RT_INFINITY, t)) return 0.0f;
-    float4 A = sp[0], B = sp[1];
+    float4 A = ldg(sp), B = ldg(sp + 1);
     v3 pc = sub3(f3(A), o);
     float d2 = g_dot(pc, pc);
     float ctm = sqrtf(1.0f - B.w * B.w / d2);
@@ -901,12 +1053,12 @@ __device__ __forceinline__ float quad_light_pdf(const KP& P, int idx, v3 o, v3 d
     const float4* q = reinterpret_cast<const float4*>(P.quads + idx);
     float t, al, be;
     if (!quad_test(P.dquads + RT_DFACE_F4 * idx, o, d, 0.001f, RT_INFINITY, t, al, be)) return 0.0f;
-    v3 n = f3(q[0]);
+    v3 n = f3(ldg(q));
     bool front = g_dot(d, n) < 0.0f;
     v3 normal = front ? n : neg3(n);
     float d2 = t * t * g_dot(d, d);
     float cosine = fabsf(g_dot(d, normal) / g_length(d));
-    return d2 / (cosine * q[3].w);
+    return d2 / (cosine * ldg(q + 3).w);
 }
 
 // pdf.glsl:58-81
@@ -914,7 +1066,7 @@ __device__ __forceinline__ float lights_pdf_value(const KP& P, v3 o, v3 d, float
     float weight = 1.0f / (float)P.lights_count;
     float sum = 0.0f;
     for (int i = 0; i < P.lights_count; i++) {
-        int packed = P.lights[i];
+        int packed = ldg_i(P.lights + i);
         int type = (packed >> 16) & 0xFFFF, idx = packed & 0xFFFF;
         float pdf = 0.0f;
         if (type == RT_MODEL_SPHERE) pdf = sphere_light_pdf(P, idx, o, d, time);
@@ -929,11 +1081,11 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, float& rf, float 
     float r = 0.0f + rnd(rf, px, py) * ((float)(P.lights_count - 1 + 1) - 0.0f);
     int li = rt_f2i(floorf(r));
     if (li < 0 || li >= P.lights_count) return mk3s(0.0f);
-    int packed = P.lights[li];
+    int packed = ldg_i(P.lights + li);
     int type = (packed >> 16) & 0xFFFF, idx = packed & 0xFFFF;
     if (type == RT_MODEL_SPHERE) {
         const float4* sp = reinterpret_cast<const float4*>(P.spheres + idx);
-        float4 A = sp[0], B = sp[1];
+        float4 A = ldg(sp), B = ldg(sp + 1);
         v3 dir = sub3(f3(A), o);
         float d2 = g_dot(dir, dir);
         float r1 = rnd(rf, px, py);
@@ -948,7 +1100,7 @@ __device__ __forceinline__ v3 lights_random(const KP& P, v3 o, float& rf, float 
     }
     if (type == RT_MODEL_QUAD) {
         const float4* q = reinterpret_cast<const float4*>(P.quads + idx);
-        float4 Q1 = q[1], Q2 = q[2], Q3 = q[3];
+        float4 Q1 = ldg(q + 1), Q2 = ldg(q + 2), Q3 = ldg(q + 3);
         float r1 = rnd(rf, px, py);
         v3 p = add3(f3(Q1), scale3(f3(Q2), r1));
         float r2 = rnd(rf, px, py);
@@ -1251,8 +1403,8 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     } else if (h.type == RT_MODEL_CONSTANT_MEDIUM) {   // hitting.glsl:189-190 + compute.glsl:211-216
         normal = mk3(1.0f, 0.0f, 0.0f);
         front = true;
-        material = P.media[h.idx].phase_material;
-        tex_id = P.media[h.idx].texture_id;
+        material = ldg_i(&P.media[h.idx].phase_material);
+        tex_id = ldg_i(&P.media[h.idx].texture_id);
     } else {   // quad, or box face h.face (material from quads[0], compute.glsl:217-221)
         const float4* q0 = (h.type == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + h.idx)
                                                     : reinterpret_cast<const float4*>(P.boxes + h.idx);
@@ -1652,6 +1804,8 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
     const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
     const int batch = P.sm_batch;
+    // RT_OPT_COMPACT: the wave's share of the running-mean LDS slots (64 float4, unused here)
+    float4* const cslots = rt_dyn_lds + P.acc_lds + (threadIdx.x & ~63u);
     // wave-uniform: the units in the two slots (-1 = free) and their stored samples;
     // the pool: its unit, slot and next unclaimed sample
     int unit0 = -1, unit1 = -1;
@@ -1815,6 +1969,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             const int n_hit = __popcll(__ballot(status == RT_SM_HIT));
             if (STATS && tr) st_pred(st, status == RT_SM_FRESH, ST_RET_IT, ST_RET_LN);
             if (tr == 0 || n_hit >= batch || n_hit * 64 >= P.sm_frac * (n_hit + __popcll(tr))) break;
+            bool at_leaf = false;   // RT_OPT_COMPACT: the lane's walk stopped at a hit leaf this round
             const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
             const bool wave_exact = __ballot(status == RT_SM_TRACE && lane_exact) != 0;
             if (status == RT_SM_TRACE) {
@@ -1833,6 +1988,8 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     // still walking: the next round goes on from nx
                 } else if (nx == RT_LINK_END) {
                     status = RT_SM_HIT;
+                } else if (OPT & RT_OPT_COMPACT) {
+                    at_leaf = true;   // tested below, with the whole wave
                 } else {
                     unsigned long long t1 = STATS ? clock64() : 0;
                     if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
@@ -1840,6 +1997,19 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     leaf_prims_t<STATS, FD>(P, lf.x, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf, fx, fy, h,
                                             has, st);
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+                    nx &= 0xFFFFu;
+                    if (nx == 0xFFFFu) status = RT_SM_HIT;
+                }
+            }
+            if ((OPT & RT_OPT_COMPACT) && __ballot(at_leaf) != 0) {
+                unsigned long long t1 = STATS ? clock64() : 0;
+                if (STATS && at_leaf) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
+                uint2 lf = make_uint2(0u, 0u);
+                if (at_leaf) lf = leaves[(nx >> 16) & 0x7FFFu];
+                leaf_round_compact<STATS, FD>(P, at_leaf, lf.x, lf.y, S.o, S.d, inv, a, S.time, tmax, S.rf, fx, fy, h,
+                                              has, cslots, st);
+                if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+                if (at_leaf) {
                     nx &= 0xFFFFu;
                     if (nx == 0xFFFFu) status = RT_SM_HIT;
                 }
@@ -2162,9 +2332,14 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
         case FAST_LDS: rc = RT_LAUNCH(false, true, true, 0); break;
         case FAST_GLOBAL: rc = RT_LAUNCH(false, false, true, 0); break;
         case LINK_LDS:
-            rc = pool && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
-                 : pool            ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM)
-                                   : RT_LAUNCH(true, true, false, 0);
+            if (pool && a.leaf_compact)
+                rc = a.fastdiv ? RT_LAUNCH(true, true, false,
+                                           RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM | RT_OPT_COMPACT)
+                               : RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM | RT_OPT_COMPACT);
+            else
+                rc = pool && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
+                     : pool            ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM)
+                                       : RT_LAUNCH(true, true, false, 0);
             break;
         case META_LDS:
             rc = pool ? RT_LAUNCH(false, true, false, RT_OPT_POOL) : RT_LAUNCH(false, true, false, 0);
