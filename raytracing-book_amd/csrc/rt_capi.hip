@@ -126,6 +126,7 @@ struct rt_ctx {
     int sm_batch = 64;   // render_stream's shading batch (env RT_SM_BATCH) ...
     int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
+    bool sph_lds = true;   // sphere records' first two float4 in LDS when they fit (env RT_SPH_LDS=0 disables; A/B)
     bool leaf_compact = false;   // render_stream: solid leaf tests compacted across the wave (env RT_LEAF_COMPACT)
     size_t sample_budget = (size_t)32 << 30;
 };
@@ -772,6 +773,7 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_SM_FRAC")) c->sm_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_WALK_FRAC")) c->walk_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_LEAF_COMPACT")) c->leaf_compact = std::atoi(v) != 0;
+    if (const char* v = std::getenv("RT_SPH_LDS")) c->sph_lds = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
@@ -1140,6 +1142,19 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                             (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] / 4 : 0);
         if (a.n_media > 0 && a.n_media <= 64 && shape_p && (base + 3 * (size_t)a.n_media) * 16 <= lds_cap)
             a.media_lds = (int)base;
+    }
+    // the spheres' (A, B) after them, for the pooled link-walk kernel (variant 0 / 39): the leaf
+    // tests' sphere loads become LDS reads when the whole set fits the shape's budget
+    a.sph_lds = -1;
+    a.n_sph_lds = (int)(c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere));
+    {
+        const size_t base = (a.media_lds >= 0) ? (size_t)a.media_lds + 3 * (size_t)a.n_media
+                            : node_f4 + (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] *
+                                                                 c->tex_h[a.perlin_slot] / 4
+                                                           : 0);
+        if (c->sph_lds && links && (c->variant == 0 || c->variant == 39) && a.n_sph_lds > 0 &&
+            (base + 2 * (size_t)a.n_sph_lds) * 16 <= lds_cap)
+            a.sph_lds = (int)base;
     }
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);

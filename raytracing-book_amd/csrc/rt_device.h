@@ -116,6 +116,8 @@ struct rt_kernel_args {
     int n_media;
     int media_lds;               // float4 offset of the media records + sphere boundaries in LDS (3 float4
                                  // per medium, after the Perlin table), or -1
+    int sph_lds;                 // float4 offset of the spheres' intersection halves (A, B) in LDS, or -1
+    int n_sph_lds;               // spheres staged there
     int acc_lds;                 // float4 offset of the lanes' running-mean slots (after everything staged)
     // exact near-first walk (variant 61; tables from rt_capi.hip build_fast)
     const uint32_t* finfo;       // per solid prim (finfo_base[type] + index): reference rank << 16 | reference leaf

@@ -512,8 +512,13 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
         bool hit = false;
         unsigned long long c0 = STATS ? clock64() : 0;
         if (ty == RT_MODEL_SPHERE) {
-            hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t, fd,
-                           fd ? rcp_nr(a) : 0.0f);
+            if (P.sph_lds >= 0) {   // the record's intersection half from LDS (render_persistent)
+                const float4* r = rt_dyn_lds + P.sph_lds + 2 * ix;
+                hit = sphere_t_ab(r[0], r[1], time, o, d, a, tmin, tmax, t, fd, fd ? rcp_nr(a) : 0.0f);
+            } else {
+                hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t, fd,
+                               fd ? rcp_nr(a) : 0.0f);
+            }
             if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
             if (STATS) st_add(st, ST_SPH_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_QUAD) {
@@ -2114,6 +2119,10 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
                 s_nodes[P.media_lds + k] = v;
             }
         }
+        if (P.sph_lds >= 0) {   // per sphere its first two float4 (center0 + texture, motion + radius)
+            const float4* sp = reinterpret_cast<const float4*>(P.spheres);
+            for (int k = tid; k < 2 * P.n_sph_lds; k += BLOCK) s_nodes[P.sph_lds + k] = ldg(sp + (k >> 1) * 3 + (k & 1));
+        }
     }
     // per lane: the pixel's running mean during a unit, after what this launch
     // shape stages (P.acc_lds, set by rt_launch_render with the LDS size)
@@ -2277,7 +2286,8 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     const bool fits_t = lds_t <= RT_LDS_NODE_BYTES;
     // after the nodes, as placed by the host: the Perlin table, then the media records
     const size_t extra_end =
-        a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
+        a.sph_lds >= 0 ? ((size_t)a.sph_lds + 2 * (size_t)a.n_sph_lds) * 16
+        : a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
         : a.perlin_lds >= 0 ? ((size_t)a.perlin_lds + ((size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h + 3) / 4) * 16
                             : 0;
     const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
