@@ -126,8 +126,8 @@ struct rt_ctx {
     int sm_batch = 64;   // render_stream's shading batch (env RT_SM_BATCH) ...
     int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
+    bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
     bool sph_lds = true;   // sphere records' first two float4 in LDS when they fit (env RT_SPH_LDS=0 disables; A/B)
-    bool leaf_compact = false;   // render_stream: solid leaf tests compacted across the wave (env RT_LEAF_COMPACT)
     size_t sample_budget = (size_t)32 << 30;
 };
 
@@ -772,8 +772,8 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_SM_BATCH")) c->sm_batch = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SM_FRAC")) c->sm_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_WALK_FRAC")) c->walk_frac = std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RT_LEAF_COMPACT")) c->leaf_compact = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_SPH_LDS")) c->sph_lds = std::atoi(v) != 0;
+    if (const char* v = std::getenv("RT_BIG_WG")) c->big_wg = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
@@ -1104,7 +1104,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.sm_batch = c->sm_batch;
     a.sm_frac = c->sm_frac;
     a.walk_frac = c->walk_frac;
-    a.leaf_compact = c->leaf_compact ? 1 : 0;
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);
@@ -1127,7 +1126,30 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     const bool links = !fast_walk && c->variant != 30 && c->variant != 31 && a.n_lnode_f4 > 0;
     const bool shape_p = !fast_walk;
     const size_t node_f4 = links ? (size_t)a.n_lnode_f4 : (size_t)2 * c->n_dnodes;
-    const size_t lds_cap = links ? RT_LDS_DYN_BYTES : RT_LDS_NODE_BYTES;
+    size_t lds_cap = links ? RT_LDS_DYN_BYTES : RT_LDS_NODE_BYTES;
+    // The pooled link-walk kernel (variant 0 / 39) runs as one 1024-thread workgroup per CU
+    // when everything below (with the spheres' and the canonical boxes' leaf-test records)
+    // fits RT_LDS_BIG_BYTES and some of it would not fit the 512-thread shape.
+    const bool pooled_link = links && (c->variant == 0 || c->variant == 39);
+    const int n_sph = (int)(c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere));
+    const int n_box = (int)(c->host_buf[RT_BIND_BOXES].size() / sizeof(rt_box));
+    const int n_med = (int)(c->host_buf[RT_BIND_MEDIA].size() / sizeof(rt_medium));
+    a.block = 512;
+    if (pooled_link && c->big_wg) {
+        size_t perlin_f4 = 0;
+        for (int t = 0; t < RT_MAX_TEXTURES; t++)
+            if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) {
+                perlin_f4 = (size_t)c->tex_w[t] * c->tex_h[t] / 4;
+                break;
+            }
+        const size_t box_f4 = (c->boxes_canon && c->sph_lds) ? 5 * (size_t)n_box : 0;
+        const size_t all_f4 = node_f4 + perlin_f4 + (n_med <= 64 ? 3 * (size_t)n_med : 0) +
+                              (c->sph_lds ? 2 * (size_t)n_sph : 0) + box_f4;
+        if (all_f4 * 16 <= RT_LDS_BIG_BYTES && all_f4 * 16 > RT_LDS_DYN_BYTES) {
+            a.block = 1024;
+            lds_cap = RT_LDS_BIG_BYTES;
+        }
+    }
     a.perlin_slot = a.perlin_lds = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
@@ -1144,17 +1166,21 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             a.media_lds = (int)base;
     }
     // the spheres' (A, B) after them, for the pooled link-walk kernel (variant 0 / 39): the leaf
-    // tests' sphere loads become LDS reads when the whole set fits the shape's budget
-    a.sph_lds = -1;
-    a.n_sph_lds = (int)(c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere));
+    // tests' sphere loads become LDS reads when the whole set fits the shape's budget; then,
+    // in the 1024-thread shape, the canonical boxes' bounds and planes
+    a.sph_lds = a.box_lds = -1;
+    a.n_sph_lds = n_sph;
+    a.n_box_lds = n_box;
     {
-        const size_t base = (a.media_lds >= 0) ? (size_t)a.media_lds + 3 * (size_t)a.n_media
-                            : node_f4 + (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] *
-                                                                 c->tex_h[a.perlin_slot] / 4
-                                                           : 0);
-        if (c->sph_lds && links && (c->variant == 0 || c->variant == 39) && a.n_sph_lds > 0 &&
-            (base + 2 * (size_t)a.n_sph_lds) * 16 <= lds_cap)
+        size_t base = (a.media_lds >= 0) ? (size_t)a.media_lds + 3 * (size_t)a.n_media
+                      : node_f4 + (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] / 4
+                                                     : 0);
+        if (c->sph_lds && pooled_link && n_sph > 0 && (base + 2 * (size_t)n_sph) * 16 <= lds_cap) {
             a.sph_lds = (int)base;
+            base += 2 * (size_t)n_sph;
+        }
+        if (a.block == 1024 && c->boxes_canon && c->sph_lds && n_box > 0 && (base + 5 * (size_t)n_box) * 16 <= lds_cap)
+            a.box_lds = (int)base;
     }
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);

@@ -35,6 +35,10 @@
 // slots (RT_LDS_ACC_BYTES), all in the dynamic region (no static LDS)
 #define RT_LDS_ACC_BYTES (512 * 16)
 #define RT_LDS_DYN_BYTES (80 * 1024 - RT_LDS_ACC_BYTES)   // link nodes + Perlin + media, or variant 61's tree + stacks
+// the pooled link-walk kernel as one 1024-thread workgroup per CU (16 waves, 4 per SIMD as
+// two of 512): one copy of the nodes per CU leaves room for the leaf tests' sphere and box
+// records; 8 KB of the 160 KB stay for the stats build's static counters
+#define RT_LDS_BIG_BYTES (152 * 1024)
 #define RT_LDS_NODE_BYTES (64 * 1024)   // threaded (meta-word) nodes in LDS when they fit
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
@@ -103,7 +107,6 @@ struct rt_kernel_args {
     int sm_frac;                 // or this many 64ths of the lanes with a walk (or none runs)
     int walk_frac;               // render_sm: a round's node walk stops once this many 64ths of its lanes
                                  // hold a leaf or ended (64: all of them)
-    int leaf_compact;            // render_stream: a round's solid leaf tests compacted across the wave
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
@@ -118,6 +121,10 @@ struct rt_kernel_args {
                                  // per medium, after the Perlin table), or -1
     int sph_lds;                 // float4 offset of the spheres' intersection halves (A, B) in LDS, or -1
     int n_sph_lds;               // spheres staged there
+    int box_lds;                 // float4 offset of the canonical boxes' bounds + planes (5 float4 each) in LDS, or -1
+    int n_box_lds;               // boxes staged there
+    int block;                   // the render kernel's workgroup size: 512, or 1024 (one per CU) when the
+                                 // records above fit its LDS (RT_LDS_BIG_BYTES)
     int acc_lds;                 // float4 offset of the lanes' running-mean slots (after everything staged)
     // exact near-first walk (variant 61; tables from rt_capi.hip build_fast)
     const uint32_t* finfo;       // per solid prim (finfo_base[type] + index): reference rank << 16 | reference leaf

@@ -41,7 +41,6 @@ typedef rt_kernel_args KP;
 #define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_stream)
 #define RT_OPT_FD 4     // with RT_OPT_SM: the scene is in the shared-reciprocal division regime (P.fastdiv)
 #define RT_OPT_STREAM 8 // with RT_OPT_SM: the wave streams over units (render_stream) instead of one at a time
-#define RT_OPT_COMPACT 16 // with RT_OPT_STREAM: a round's solid leaf tests compacted across the wave (leaf_round_compact)
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -284,10 +283,10 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
 // pair of faces divides by +-(s * d_k), so one reciprocal per axis, negated for the
 // opposite face; a plane t is kept only when >= tmin = 0.001, never in the
 // tiny-numerator case.
-__device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, const float4* __restrict__ fb, v3 o,
-                                               v3 d, float tmin, float tmax, float& t, int& face, float& alpha,
-                                               float& beta, bool fd = false) {
-    const float4 c0 = ldg(pl), c1 = ldg(pl + 1), c2 = ldg(pl + 2);
+// c0..c2: the record's canonical planes (fb[18..20], from global memory or LDS).
+__device__ __forceinline__ bool box_test_canon_c(float4 c0, float4 c1, float4 c2, const float4* __restrict__ fb, v3 o,
+                                                 v3 d, float tmin, float tmax, float& t, int& face, float& alpha,
+                                                 float& beta, bool fd = false) {
     const float sv[6] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z};
     const float wv[6] = {c0.y, c0.w, c1.y, c1.w, c2.y, c2.w};
     const float dk[6] = {d.z, d.x, d.z, d.x, d.y, d.y};
@@ -330,6 +329,11 @@ __device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, co
         }
     }
     return has;
+}
+__device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, const float4* __restrict__ fb, v3 o,
+                                               v3 d, float tmin, float tmax, float& t, int& face, float& alpha,
+                                               float& beta, bool fd = false) {
+    return box_test_canon_c(ldg(pl), ldg(pl + 1), ldg(pl + 2), fb, o, d, tmin, tmax, t, face, alpha, beta, fd);
 }
 
 // hitting.glsl:148-160 for a medium boundary (only rec.t is read, :165-178).
@@ -527,18 +531,32 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             if (STATS) st_add(st, ST_QUAD_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_BOX) {
             const float4* rec = P.dboxes + RT_DBOX_F4 * ix;
+            // LDS copy (P.box_lds >= 0, canonical boxes): bounds, then the canonical planes
+            const float4* lb = rt_dyn_lds + P.box_lds + 5 * ix;
             bool maybe = true;
             if (P.box_margin > 0.0f && fin) {
                 // the box's bounds grown by box_margin (rt_device.h): a ray that misses them
                 // misses every face the exact test below would accept
                 const float m = P.box_margin;
-                const float4 b0 = ldg(rec + 21), b1 = ldg(rec + 22);
+                float4 b0, b1;
+                if (P.box_lds >= 0) {
+                    b0 = lb[0];
+                    b1 = lb[1];
+                } else {
+                    b0 = ldg(rec + 21);
+                    b1 = ldg(rec + 22);
+                }
                 maybe = aabb_pk(make_float4(b0.x - m, b0.y + m, b0.z - m, b0.w + m),
                                 make_float4(b1.x - m, b1.y + m, 0.0f, 0.0f), o, inv, tmin, tmax);
             }
-            if (maybe)
-                hit = (P.boxes_canon && fin) ? box_test_canon(rec + 18, rec, o, d, tmin, tmax, t, face, al, be, fd)
-                                             : box_test(rec, o, d, tmin, tmax, t, face, al, be, fd);
+            if (maybe) {
+                if (P.boxes_canon && fin)
+                    hit = P.box_lds >= 0
+                              ? box_test_canon_c(lb[2], lb[3], lb[4], rec, o, d, tmin, tmax, t, face, al, be, fd)
+                              : box_test_canon(rec + 18, rec, o, d, tmin, tmax, t, face, al, be, fd);
+                else
+                    hit = box_test(rec, o, d, tmin, tmax, t, face, al, be, fd);
+            }
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
@@ -549,147 +567,6 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             has = true;
             tmax = t;
             h.t = t; h.type = ty; h.idx = ix; h.face = face;
-        }
-    }
-}
-
-// Lanes of this wave whose bit in m is set below this lane (v_mbcnt).
-__device__ __forceinline__ int lanes_below(unsigned long long m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ float pull(float v, int addr) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
-}
-__device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
-
-// One round's leaf tests (compute.glsl:247-256) with the solid prims' tests
-// compacted across the wave (RT_OPT_COMPACT; called with every lane of the wave
-// active).  leaf_prims_t runs each prim type's code once per slot whenever any
-// lane has that type there: per round, box code ran 1.68 times at 17 of 64 lanes
-// and sphere code 1.19 times at 10 (profiles/r02_region_stats_s8.log).  Here the
-// round's sphere / quad / box tests of both slots form one list (boxes, spheres,
-// quads; per type slot 0 then slot 1), and lane k of the wave runs test k on its
-// owner's ray (ds_bpermute), so each type's code runs once per 64 tests.
-// Exact: a solid's result does not depend on the order of the leaf's tests except
-// through ray_t.max, and a test run with the round's ray_t.max gives the sequential
-// test's result under any smaller max m' iff its t passes m' (sphere: t < m'; the
-// larger root is >= the smaller one, so a root that fails m' leaves none; box: the
-// accepted face is the last one with the least t among the faces in range, which
-// stays the accepted one while its t <= m'; quad: one face).  So each lane applies
-// its slots in order: a solid's result against its running max, a medium's test
-// (rand() draws depend on the running max) in the lane itself, as the reference.
-// The wave's 1 KB of the lanes' running-mean LDS slots (unused by render_stream)
-// carries the test list and the results.
-template <bool STATS, bool FD>
-__device__ __forceinline__ void leaf_round_compact(const KP& P, bool at_leaf, uint32_t meta, uint32_t prims, v3 o,
-                                                   v3 d, v3 inv, float a, float time, float& tmax, float& rf,
-                                                   float px, float py, Hit& h, bool& has, float4* slots,
-                                                   unsigned long long* st) {
-    constexpr bool fd = FD;
-    const int lane = (int)__lane_id();
-    const int ty0 = at_leaf ? (int)((meta >> 16) & 0xFu) : 0;
-    const int ty1 = at_leaf ? (int)((meta >> 20) & 0xFu) : 0;
-    const int ix0 = (int)(prims & 0xFFFFu), ix1 = (int)(prims >> 16);
-    const unsigned long long b0 = __ballot(ty0 == RT_MODEL_BOX), b1 = __ballot(ty1 == RT_MODEL_BOX);
-    const unsigned long long s0 = __ballot(ty0 == RT_MODEL_SPHERE), s1 = __ballot(ty1 == RT_MODEL_SPHERE);
-    const unsigned long long q0 = __ballot(ty0 == RT_MODEL_QUAD), q1 = __ballot(ty1 == RT_MODEL_QUAD);
-    const int nb0 = __popcll(b0), nb = nb0 + __popcll(b1);
-    const int ns0 = __popcll(s0), ns = ns0 + __popcll(s1);
-    const int nq0 = __popcll(q0), n = nb + ns + nq0 + __popcll(q1);
-    int pos0 = -1, pos1 = -1;
-    if (ty0 == RT_MODEL_BOX) pos0 = lanes_below(b0);
-    else if (ty0 == RT_MODEL_SPHERE) pos0 = nb + lanes_below(s0);
-    else if (ty0 == RT_MODEL_QUAD) pos0 = nb + ns + lanes_below(q0);
-    if (ty1 == RT_MODEL_BOX) pos1 = nb0 + lanes_below(b1);
-    else if (ty1 == RT_MODEL_SPHERE) pos1 = nb + ns0 + lanes_below(s1);
-    else if (ty1 == RT_MODEL_QUAD) pos1 = nb + ns + nq0 + lanes_below(q1);
-    float4 r0 = make_float4(-1.0f, 0.0f, 0.0f, 0.0f), r1 = r0;
-    int* const sw = reinterpret_cast<int*>(slots);
-    for (int p = 0; p < n; p += 64) {   // wave-uniform; one pass unless the round has > 64 tests
-        // owners post their tests: prim index | type << 16 | owner lane << 20
-        if ((unsigned)(pos0 - p) < 64u) sw[4 * (pos0 - p) + 3] = ix0 | (ty0 << 16) | (lane << 20);
-        if ((unsigned)(pos1 - p) < 64u) sw[4 * (pos1 - p) + 3] = ix1 | (ty1 << 16) | (lane << 20);
-        wave_lds_fence();
-        const bool ex = lane < n - p;
-        int dsc = lane << 20;
-        if (ex) dsc = sw[4 * lane + 3];
-        // the owner's ray, pulled with every lane active (ds_bpermute reads active lanes only)
-        const int src = ((dsc >> 20) & 63) << 2;
-        const v3 eo = mk3(pull(o.x, src), pull(o.y, src), pull(o.z, src));
-        const v3 ed = mk3(pull(d.x, src), pull(d.y, src), pull(d.z, src));
-        const v3 ei = mk3(pull(inv.x, src), pull(inv.y, src), pull(inv.z, src));
-        const float etmax = pull(tmax, src), ea = pull(a, src), etime = pull(time, src);
-        if (ex) {
-            const int ety = (dsc >> 16) & 0xF, eix = dsc & 0xFFFF;
-            float t = 0.0f, al = 0.0f, be = 0.0f;
-            int face = 0;
-            bool hit = false;
-            if (STATS) {
-                st_pred(st, ety == RT_MODEL_SPHERE, ST_SPH_IT, ST_SPH_LN);
-                st_pred(st, ety == RT_MODEL_QUAD, ST_QUAD_IT, ST_QUAD_LN);
-                st_pred(st, ety == RT_MODEL_BOX, ST_BOX_IT, ST_BOX_LN);
-            }
-            unsigned long long c0 = STATS ? clock64() : 0;
-            if (ety == RT_MODEL_BOX) {
-                const bool fin = fabsf(eo.x) < INFINITY && fabsf(eo.y) < INFINITY && fabsf(eo.z) < INFINITY &&
-                                 fabsf(ed.x) < INFINITY && fabsf(ed.y) < INFINITY && fabsf(ed.z) < INFINITY;
-                const float4* rec = P.dboxes + RT_DBOX_F4 * eix;
-                bool maybe = true;
-                if (P.box_margin > 0.0f && fin) {   // leaf_prims_t's bounds pre-test
-                    const float m = P.box_margin;
-                    const float4 bb0 = ldg(rec + 21), bb1 = ldg(rec + 22);
-                    maybe = aabb_pk(make_float4(bb0.x - m, bb0.y + m, bb0.z - m, bb0.w + m),
-                                    make_float4(bb1.x - m, bb1.y + m, 0.0f, 0.0f), eo, ei, 0.001f, etmax);
-                }
-                if (maybe)
-                    hit = (P.boxes_canon && fin)
-                              ? box_test_canon(rec + 18, rec, eo, ed, 0.001f, etmax, t, face, al, be, fd)
-                              : box_test(rec, eo, ed, 0.001f, etmax, t, face, al, be, fd);
-                if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
-            } else if (ety == RT_MODEL_SPHERE) {
-                hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + eix), etime, eo, ed, ea, 0.001f, etmax, t,
-                               fd, fd ? rcp_nr(ea) : 0.0f);
-                if (STATS) st_add(st, ST_SPH_CYC, clock64() - c0);
-            } else {
-                hit = quad_test(P.dquads + RT_DFACE_F4 * eix, eo, ed, 0.001f, etmax, t, al, be, fd);
-                if (STATS) st_add(st, ST_QUAD_CYC, clock64() - c0);
-            }
-            slots[lane] = make_float4(hit ? t : -1.0f, al, be, __int_as_float(face));
-        }
-        wave_lds_fence();
-        if ((unsigned)(pos0 - p) < 64u) r0 = slots[pos0 - p];
-        if ((unsigned)(pos1 - p) < 64u) r1 = slots[pos1 - p];
-        wave_lds_fence();
-    }
-    // each lane's slots in order against its running ray_t.max
-#pragma unroll 1
-    for (int s = 0; s < 2; s++) {
-        const int ty = s ? ty1 : ty0, ix = s ? ix1 : ix0;
-        const float4 r = s ? r1 : r0;
-        float t = r.x;
-        bool hit;
-        if (STATS) st_pred(st, ty == RT_MODEL_CONSTANT_MEDIUM, ST_MED_IT, ST_MED_LN);
-        if (ty == RT_MODEL_CONSTANT_MEDIUM) {
-            unsigned long long c0 = STATS ? clock64() : 0;
-            hit = medium_test(P, ix, o, d, a, time, 0.001f, tmax, rf, px, py, t);
-            if (STATS) st_add(st, ST_MED_CYC, clock64() - c0);
-        } else {
-            hit = t >= 0.0f && (ty == RT_MODEL_SPHERE ? t < tmax : t <= tmax);   // t = -1: no hit (or no test)
-        }
-        if (hit) {
-            has = true;
-            tmax = t;
-            h.t = t; h.type = ty; h.idx = ix; h.face = __float_as_int(r.w);
-            if (ty == RT_MODEL_SPHERE) {
-                h.uv_kind_idx = (1 << 16) | ix;
-                h.uv_a = t;
-            } else if (ty != RT_MODEL_CONSTANT_MEDIUM) {
-                h.uv_kind_idx = 2 << 16;
-                h.uv_a = r.y;
-                h.uv_b = r.z;
-            } else {
-                h.face = 0;
-            }
         }
     }
 }
@@ -1809,8 +1686,6 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
     const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
     const int batch = P.sm_batch;
-    // RT_OPT_COMPACT: the wave's share of the running-mean LDS slots (64 float4, unused here)
-    float4* const cslots = rt_dyn_lds + P.acc_lds + (threadIdx.x & ~63u);
     // wave-uniform: the units in the two slots (-1 = free) and their stored samples;
     // the pool: its unit, slot and next unclaimed sample
     int unit0 = -1, unit1 = -1;
@@ -1974,7 +1849,6 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             const int n_hit = __popcll(__ballot(status == RT_SM_HIT));
             if (STATS && tr) st_pred(st, status == RT_SM_FRESH, ST_RET_IT, ST_RET_LN);
             if (tr == 0 || n_hit >= batch || n_hit * 64 >= P.sm_frac * (n_hit + __popcll(tr))) break;
-            bool at_leaf = false;   // RT_OPT_COMPACT: the lane's walk stopped at a hit leaf this round
             const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
             const bool wave_exact = __ballot(status == RT_SM_TRACE && lane_exact) != 0;
             if (status == RT_SM_TRACE) {
@@ -1993,8 +1867,6 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     // still walking: the next round goes on from nx
                 } else if (nx == RT_LINK_END) {
                     status = RT_SM_HIT;
-                } else if (OPT & RT_OPT_COMPACT) {
-                    at_leaf = true;   // tested below, with the whole wave
                 } else {
                     unsigned long long t1 = STATS ? clock64() : 0;
                     if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
@@ -2002,19 +1874,6 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     leaf_prims_t<STATS, FD>(P, lf.x, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf, fx, fy, h,
                                             has, st);
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-                    nx &= 0xFFFFu;
-                    if (nx == 0xFFFFu) status = RT_SM_HIT;
-                }
-            }
-            if ((OPT & RT_OPT_COMPACT) && __ballot(at_leaf) != 0) {
-                unsigned long long t1 = STATS ? clock64() : 0;
-                if (STATS && at_leaf) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-                uint2 lf = make_uint2(0u, 0u);
-                if (at_leaf) lf = leaves[(nx >> 16) & 0x7FFFu];
-                leaf_round_compact<STATS, FD>(P, at_leaf, lf.x, lf.y, S.o, S.d, inv, a, S.time, tmax, S.rf, fx, fy, h,
-                                              has, cslots, st);
-                if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-                if (at_leaf) {
                     nx &= 0xFFFFu;
                     if (nx == 0xFFFFu) status = RT_SM_HIT;
                 }
@@ -2122,6 +1981,12 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         if (P.sph_lds >= 0) {   // per sphere its first two float4 (center0 + texture, motion + radius)
             const float4* sp = reinterpret_cast<const float4*>(P.spheres);
             for (int k = tid; k < 2 * P.n_sph_lds; k += BLOCK) s_nodes[P.sph_lds + k] = ldg(sp + (k >> 1) * 3 + (k & 1));
+        }
+        if (P.box_lds >= 0) {   // per canonical box: bounds (fb[21..22]), canonical planes (fb[18..20])
+            for (int k = tid; k < 5 * P.n_box_lds; k += BLOCK) {
+                const int b = k / 5, j = k - 5 * b;
+                s_nodes[P.box_lds + k] = ldg(P.dboxes + RT_DBOX_F4 * b + (j < 2 ? 21 + j : 16 + j));
+            }
         }
     }
     // per lane: the pixel's running mean during a unit, after what this launch
@@ -2286,7 +2151,8 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     const bool fits_t = lds_t <= RT_LDS_NODE_BYTES;
     // after the nodes, as placed by the host: the Perlin table, then the media records
     const size_t extra_end =
-        a.sph_lds >= 0 ? ((size_t)a.sph_lds + 2 * (size_t)a.n_sph_lds) * 16
+        a.box_lds >= 0 ? ((size_t)a.box_lds + 5 * (size_t)a.n_box_lds) * 16
+        : a.sph_lds >= 0 ? ((size_t)a.sph_lds + 2 * (size_t)a.n_sph_lds) * 16
         : a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
         : a.perlin_lds >= 0 ? ((size_t)a.perlin_lds + ((size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h + 3) / 4) * 16
                             : 0;
@@ -2304,7 +2170,8 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.variant == 61 || a.variant == 69) {
         shape = tree_b + stack_b <= RT_LDS_DYN_BYTES ? FAST_LDS : FAST_GLOBAL;
         staged = shape == FAST_LDS ? tree_b + stack_b : stack_b;
-    } else if (a.variant != 30 && a.variant != 31 && a.n_lnode_f4 > 0 && lds_l <= RT_LDS_DYN_BYTES) {
+    } else if (a.variant != 30 && a.variant != 31 && a.n_lnode_f4 > 0 &&
+               lds_l <= (a.block == 1024 ? RT_LDS_BIG_BYTES : RT_LDS_DYN_BYTES)) {
         shape = LINK_LDS;
         staged = lds_l;
     } else if (fits_t && lds_p <= RT_LDS_DYN_BYTES) {
@@ -2314,8 +2181,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
         shape = META_GLOBAL;
         staged = 0;
     }
+    const bool big = shape == LINK_LDS && pool && a.block == 1024;   // render_stream needs no running-mean slots
     a.acc_lds = (int)(staged / 16);
-    const size_t lds = staged + acc;
+    const size_t lds = staged + (big ? 0 : acc);
     static const bool log_shape = std::getenv("RT_LOG_SHAPE") != nullptr;   // diagnostics: the chosen launch shape
     if (log_shape)
         std::fprintf(stderr, "rt_launch_render: shape %d (0 fast-lds 1 fast-global 2 link 3 meta-lds 4 meta-global), "
@@ -2337,19 +2205,21 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
 #define RT_LAUNCH(LINK, LDSN, FAST, OPT)                                                                        \
     (stats ? launch_persistent(render_persistent<LINK, 4, true, LDSN, 512, FAST, OPT>, 512, lds, a, d, st)    \
            : launch_persistent(render_persistent<LINK, 4, false, LDSN, 512, FAST, OPT>, 512, lds, a, d, st))
+#define RT_LAUNCH_BIG(OPT)                                                                                       \
+    (stats ? launch_persistent(render_persistent<true, 4, true, true, 1024, false, OPT>, 1024, lds, a, d, st)  \
+           : launch_persistent(render_persistent<true, 4, false, true, 1024, false, OPT>, 1024, lds, a, d, st))
     int rc;
     switch (shape) {
         case FAST_LDS: rc = RT_LAUNCH(false, true, true, 0); break;
         case FAST_GLOBAL: rc = RT_LAUNCH(false, false, true, 0); break;
         case LINK_LDS:
-            if (pool && a.leaf_compact)
-                rc = a.fastdiv ? RT_LAUNCH(true, true, false,
-                                           RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM | RT_OPT_COMPACT)
-                               : RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM | RT_OPT_COMPACT);
+            if (big)
+                rc = a.fastdiv ? RT_LAUNCH_BIG(RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
+                               : RT_LAUNCH_BIG(RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM);
             else
-                rc = pool && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
-                     : pool            ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM)
-                                       : RT_LAUNCH(true, true, false, 0);
+            rc = pool && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
+                 : pool            ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM)
+                                   : RT_LAUNCH(true, true, false, 0);
             break;
         case META_LDS:
             rc = pool ? RT_LAUNCH(false, true, false, RT_OPT_POOL) : RT_LAUNCH(false, true, false, 0);
@@ -2359,6 +2229,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
             break;
     }
 #undef RT_LAUNCH
+#undef RT_LAUNCH_BIG
     if (rc) return rc;
     if (a.samples) {   // staged chunks: the running mean over the launch's frames
         const unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);

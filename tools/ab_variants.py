@@ -4,7 +4,7 @@ Every variant must produce the same bits; timings are HIP-event device time of
 one rt_render call (1 launch) per round, reported as median/min over rounds.
 A variant spec is "<RT_KERNEL_VARIANT>" optionally followed by c<RT_CHUNK_TARGET>,
 k<RT_SHADE_K>, d<RT_DEBUG_FLAGS> (ablations: bits differ by design) and/or
-s<RT_STAGE_TILES>, b<RT_SM_BATCH>, f<RT_SM_FRAC>, x<RT_FASTDIV>, w<RT_WALK_FRAC>, p<RT_BOX_PRETEST>, t<RT_STAGED_CHUNK_TARGET>, l<RT_LEAF_COMPACT>, h<RT_SPH_LDS> (e.g. 30c0 = variant 30 with one unit per tile; 0s0 = ordered
+s<RT_STAGE_TILES>, b<RT_SM_BATCH>, f<RT_SM_FRAC>, x<RT_FASTDIV>, w<RT_WALK_FRAC>, p<RT_BOX_PRETEST>, t<RT_STAGED_CHUNK_TARGET>, h<RT_SPH_LDS>, g<RT_BIG_WG> (e.g. 30c0 = variant 30 with one unit per tile; 0s0 = ordered
 chunks whatever the tile count; 0s1000 = staged chunks).
 usage: python tools/ab_variants.py [--variants 30c0,30c16] [--rounds 5] [--scene 8]
 """
@@ -37,14 +37,14 @@ def main():
     ctxs = {}
     for v in variants:
         import re
-        m = re.fullmatch(r"(\d+)(?:c(\d+))?(?:k(\d+))?(?:d(\d+))?(?:s(\d+))?(?:b(\d+))?(?:f(\d+))?(?:x(\d+))?(?:w(\d+))?(?:p(\d+))?(?:t(\d+))?(?:l(\d+))?(?:h(\d+))?", v)
+        m = re.fullmatch(r"(\d+)(?:c(\d+))?(?:k(\d+))?(?:d(\d+))?(?:s(\d+))?(?:b(\d+))?(?:f(\d+))?(?:x(\d+))?(?:w(\d+))?(?:p(\d+))?(?:t(\d+))?(?:h(\d+))?(?:g(\d+))?", v)
         assert m, f"bad variant spec {v}"
         os.environ["RT_KERNEL_VARIANT"] = m.group(1)
         for env, val in (("RT_CHUNK_TARGET", m.group(2)), ("RT_SHADE_K", m.group(3)), ("RT_DEBUG_FLAGS", m.group(4)),
                          ("RT_STAGE_TILES", m.group(5)), ("RT_SM_BATCH", m.group(6)),
                          ("RT_SM_FRAC", m.group(7)), ("RT_FASTDIV", m.group(8)),
                          ("RT_WALK_FRAC", m.group(9)), ("RT_BOX_PRETEST", m.group(10)),
-                         ("RT_STAGED_CHUNK_TARGET", m.group(11)), ("RT_LEAF_COMPACT", m.group(12)), ("RT_SPH_LDS", m.group(13))):
+                         ("RT_STAGED_CHUNK_TARGET", m.group(11)), ("RT_SPH_LDS", m.group(12)), ("RT_BIG_WG", m.group(13))):
             if val:
                 os.environ[env] = val
             else:
