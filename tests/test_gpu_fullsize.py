@@ -116,3 +116,17 @@ def test_exactness_shortcuts_change_no_bit_1080p(gpu, monkeypatch, knob, sid):
     monkeypatch.setenv(knob, "0")
     off = render(scene, 8, 5, 4096)
     assert bit_equal(on, off), mismatch_report(on, off)
+
+
+@pytest.mark.parametrize("sid", [8, 0])
+@pytest.mark.parametrize("knob", ["RT_BIG_WG", "RT_SPH_LDS"])
+def test_lds_record_copies_change_no_bit_1080p(gpu, monkeypatch, knob, sid):
+    """The leaf tests' records read from LDS: scene 8 runs as one 1024-thread
+    workgroup per CU with its spheres' and canonical boxes' records staged beside the nodes,
+    scene 0 stages its spheres in the 512-thread shape.  Against the global-memory reads
+    (knob = 0), whole 1080p images of 8 frames: the same bits."""
+    scene = rtamd.Scene(sid, 1920, 1080, seed=1)
+    on = render(scene, 8, 5, 4096)
+    monkeypatch.setenv(knob, "0")
+    off = render(scene, 8, 5, 4096)
+    assert bit_equal(on, off), mismatch_report(on, off)
