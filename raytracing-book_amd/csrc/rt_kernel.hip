@@ -125,7 +125,7 @@ struct UvSrc {
 // Closest hit of one walk.
 struct Hit {
     float t;
-    int type, idx, face;
+    int tif;            // prim type | box face << 4 | prim index << 16 (one register)
     int uv_kind_idx;    // uv written during this walk (kind 0 = none)
     float uv_a, uv_b;   // sphere: t of that hit; quad: (alpha, beta)
 };
@@ -566,7 +566,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
         if (hit) {
             has = true;
             tmax = t;
-            h.t = t; h.type = ty; h.idx = ix; h.face = face;
+            h.t = t; h.tif = ty | (face << 4) | (ix << 16);
         }
     }
 }
@@ -1227,11 +1227,11 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
         med = mi;
     }
     if (med >= 0 && cur < best) {
-        h.t = cur; h.type = RT_MODEL_CONSTANT_MEDIUM; h.idx = med; h.face = 0;
+        h.t = cur; h.tif = RT_MODEL_CONSTANT_MEDIUM | (med << 16);
         h.uv_kind_idx = 0;
         has = true;
     } else if (best < RT_INFINITY) {
-        h.t = best; h.type = bty; h.idx = bix; h.face = bface;
+        h.t = best; h.tif = bty | (bface << 4) | (bix << 16);
         h.uv_kind_idx = (bty == RT_MODEL_SPHERE) ? ((1 << 16) | bix) : (2 << 16);
         h.uv_a = (bty == RT_MODEL_SPHERE) ? best : bal;
         h.uv_b = bbe;
@@ -1272,8 +1272,9 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     bool front;
     int material, tex_id;
     v3 emis = mk3s(0.0f);
-    if (h.type == RT_MODEL_SPHERE) {   // hitting.glsl:40-42 + compute.glsl:199-204
-        const float4* sp = reinterpret_cast<const float4*>(P.spheres + h.idx);
+    const int h_type = h.tif & 0xF, h_face = (h.tif >> 4) & 0x7, h_idx = (int)((unsigned)h.tif >> 16);
+    if (h_type == RT_MODEL_SPHERE) {   // hitting.glsl:40-42 + compute.glsl:199-204
+        const float4* sp = reinterpret_cast<const float4*>(P.spheres + h_idx);
         float4 A = ldg(sp), B = ldg(sp + 1), C = ldg(sp + 2);
         v3 center = add3(f3(A), scale3(f3(B), S.time));
         v3 on = divs3(sub3(p, center), B.w);
@@ -1282,15 +1283,15 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         material = __float_as_int(C.w);
         tex_id = __float_as_int(A.w);
         if (front) emis = f3(C);
-    } else if (h.type == RT_MODEL_CONSTANT_MEDIUM) {   // hitting.glsl:189-190 + compute.glsl:211-216
+    } else if (h_type == RT_MODEL_CONSTANT_MEDIUM) {   // hitting.glsl:189-190 + compute.glsl:211-216
         normal = mk3(1.0f, 0.0f, 0.0f);
         front = true;
-        material = ldg_i(&P.media[h.idx].phase_material);
-        tex_id = ldg_i(&P.media[h.idx].texture_id);
-    } else {   // quad, or box face h.face (material from quads[0], compute.glsl:217-221)
-        const float4* q0 = (h.type == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + h.idx)
-                                                    : reinterpret_cast<const float4*>(P.boxes + h.idx);
-        v3 n = f3(ldg(q0 + 5 * h.face));
+        material = ldg_i(&P.media[h_idx].phase_material);
+        tex_id = ldg_i(&P.media[h_idx].texture_id);
+    } else {   // quad, or box face h_face (material from quads[0], compute.glsl:217-221)
+        const float4* q0 = (h_type == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + h_idx)
+                                                    : reinterpret_cast<const float4*>(P.boxes + h_idx);
+        v3 n = f3(ldg(q0 + 5 * h_face));
         front = g_dot(d, n) < 0.0f;
         normal = front ? n : neg3(n);
         material = __float_as_int(ldg(q0 + 1).w);
@@ -1409,7 +1410,7 @@ __device__ __forceinline__ bool bounce(const KP& P, const float4* __restrict__ n
     S.depth++;
     v3 d = S.d;
     Hit h;
-    h.t = 0.0f; h.type = 0; h.idx = 0; h.face = 0;
+    h.t = 0.0f; h.tif = 0;
     h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
     // A zero direction (Q1 isotropic corner) can hit nothing and consumes no rand().
     bool dir_zero = (d.x == 0.0f) && (d.y == 0.0f) && (d.z == 0.0f);
@@ -1829,7 +1830,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
         // a new walk (bounce(): depth, a zero direction hits nothing, compute.glsl:226-229)
         if (status == RT_SM_BEGIN) {
             S.depth++;
-            h.t = 0.0f; h.type = 0; h.idx = 0; h.face = 0;
+            h.t = 0.0f; h.tif = 0;
             h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
             has = false;
             tmax = RT_INFINITY;
