@@ -319,7 +319,9 @@ def main():
     nan_px = int(np.isnan(full[..., :3]).any(axis=-1).sum())
 
     cpu = None
-    if not args.no_cpu_baseline:
+    # the CPU baseline is an N = 1 figure (rank 0 of a one-GPU run); an N-rank run skips it so
+    # the other ranks do not idle in the final barrier for a minute
+    if not args.no_cpu_baseline and world == 1:
         try:
             cpu = cpu_baseline(scene, args)
         except Exception as e:  # the baseline is reported, not required
