@@ -42,6 +42,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 FIX = json.load(open(os.path.join(HERE, "golden", "gallery.json")))
 
 LIN_TOL = 0.20
+GPU_LIN_TOL = 0.08   # 800x600, 4096 spp, max_depth 6 (test_scene8_regions_match_gallery_full_size_gpu)
 EARTH_MIN_CORR = 0.80
 
 
@@ -169,13 +170,16 @@ def test_scene8_regions_match_gallery_full_size_gpu(gpu):
     """Scene 8 at the gallery's own size (800x600) and 4096 spp through the HIP kernel
     (bit-exact with the oracle by the rest of the -m gpu suite): the fixed-geometry regions'
     means of the linearised bytes against book2_final(scene8).png, and the earth texture's
-    pattern.  At this sample count the estimate's own noise is far below LIN_TOL, so the
-    ratios printed here are the renderer's systematic distance from the published image
-    (whose spp and depth the reference does not record)."""
+    pattern.  The reference records neither the gallery's spp nor its max_depth (GUI slider
+    1-50, CLI default 5).  The blue fog region's blue channel pins the depth: 0.881 of the
+    gallery at depth 5, 1.003 at 6, 1.105 at 7 (tools/gallery_depth_probe.py,
+    profiles/r02_gallery_depth_probe.log); at depth 6 every region and channel is within
+    6.3% of the gallery (GPU_LIN_TOL = 8%), at this sample count a systematic distance, not
+    sampling noise."""
     sc = rtamd.Scene(8, 800, 600, seed=1)
     ctx = rtamd.RenderContext(devices=(0,))
     ctx.upload_scene(sc)
-    ctx.set_params(max_depth=5, spp=4096)
+    ctx.set_params(max_depth=6, spp=4096)
     ctx.resize(800, 600)
     rf = rtamd.frame_rand_factors(1, 0, 4096)
     for k in range(0, 4096, 512):
@@ -190,9 +194,9 @@ def test_scene8_regions_match_gallery_full_size_gpu(gpu):
     for name in ("glass", "metal", "blue_fog", "earth", "perlin"):
         ratio = lin[regs[name]].mean(0) / np.array(fx[name]["lin_mean"])
         report[name] = np.round(ratio, 3).tolist()
-    print("scene 8, 800x600, 4096 spp, region mean / gallery:", report)
+    print("scene 8, 800x600, 4096 spp, depth 6, region mean / gallery:", report)
     worst = max(abs(x - 1.0) for v in report.values() for x in v)
-    assert worst <= LIN_TOL, f"region mean ratio outside 1 +- {LIN_TOL}: {report}"
+    assert worst <= GPU_LIN_TOL, f"region mean ratio outside 1 +- {GPU_LIN_TOL}: {report}"
     fe = FIX["scene8_earth_blocks"]
     B = fe["block"]
     blocks = [tuple(b) for b in fe["coords"]]   # the fixture's blocks (test above: the same masks)
