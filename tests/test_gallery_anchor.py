@@ -211,3 +211,35 @@ def test_scene8_regions_match_gallery_full_size_gpu(gpu):
     corr = [float(np.corrcoef(resid(ours[:, c]), resid(gal[:, c]))[0, 1]) for c in range(3)]
     print("earth pattern correlation per channel:", np.round(corr, 3).tolist())
     assert min(corr) >= 0.95, corr   # measured 0.985-0.991 (EARTH_MIN_CORR is for 64 spp)
+
+
+@pytest.mark.gpu
+def test_scene6_blocks_match_gallery_4096spp_gpu(gpu):
+    """The Cornell box (book3_final(scene6).png, 600x600, the CLI's depth 5) at 4096 spp
+    through the HIP kernel: 60x60 block means of the PNG bytes against the gallery's, the
+    per-channel statement of the CPU suite's 64 spp oracle check (tests/test_oracle.py::
+    test_gallery_scene6) with the sampling noise gone."""
+    B = FIX["block"]
+    gb = np.array(FIX["scene6_block_means"])
+    sc = rtamd.Scene(6, FIX["width"], FIX["height"], seed=1)
+    ctx = rtamd.RenderContext(devices=(0,))
+    ctx.upload_scene(sc)
+    ctx.set_params(max_depth=5, spp=4096)
+    ctx.resize(FIX["width"], FIX["height"])
+    rf = rtamd.frame_rand_factors(1, 0, 4096)
+    for k in range(0, 4096, 512):
+        ctx.render(k + 1, rf[k:k + 512])
+    img = ctx.read_image()
+    ctx.close()
+    ours = rtamd.tonemap_rgb8(img).astype(np.float64)
+    h, w = ours.shape[:2]
+    ob = ours.reshape(h // B, B, w // B, B, 3).mean(axis=(1, 3))
+    d = ob - gb
+    corr = float(np.corrcoef(gb.ravel(), ob.ravel())[0, 1])
+    per_ch = [float(np.abs(d[..., c]).mean()) for c in range(3)]
+    print("scene 6, 600x600, 4096 spp: corr", round(corr, 5), "mean |block diff| per channel (of 255)",
+          np.round(per_ch, 3).tolist(), "max", round(float(np.abs(d).max()), 3))
+    # measured: corr 0.99998, mean |diff| 0.133 / 0.139 / 0.136 of 255, max 0.79
+    assert corr > 0.9999, corr
+    assert max(per_ch) < 0.5, per_ch
+    assert np.abs(d).max() < 2.0, np.abs(d).max()
