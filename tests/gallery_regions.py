@@ -31,6 +31,14 @@ SCENE8_MOVING = ((400.0, 400.0, 200.0), (500.0, 400.0, 200.0), 50.0)
 # the 1000-sphere cluster: centres in [0,165)^3 + (-100, 270, 395), r 10 (Scene.java:329-334)
 SCENE8_CLUSTER = ((-110.0, 260.0, 385.0), (75.0, 445.0, 570.0))
 GROUND_TOP = 101.0   # the ground boxes reach y = 1 + 100*Math.random()
+# Scene.java:44-104 (scene 0, bouncingSpheres): the three fixed spheres of radius 1; the
+# random small spheres (r 0.2 at y 0.2, some moving up by up to 0.5) stay below y = 0.9
+SCENE0_SPHERES = {
+    "glass": ((0.0, 1.0, 0.0), 1.0),        # Dielectric(1.5)
+    "diffuse": ((-4.0, 1.0, 0.0), 1.0),     # Lambertian(0.4, 0.2, 0.1)
+    "metal": ((4.0, 1.0, 0.0), 1.0),        # Metal(0.7, 0.6, 0.5; fuzz 0)
+}
+SCENE0_SMALL_TOP = 0.9
 
 
 def camera_rays(camera, width, height):
@@ -114,6 +122,31 @@ def scene8_regions(camera, width, height, erode=2):
         ok &= ~(_sphere_near(o, d, c, rm, 8.0) & (_sphere_t(o, d, c, rm + 8.0) < tbest))
     lab = np.where(ok, first, -1)
     # erode: every neighbour within `erode` pixels has the same label
+    keep = lab >= 0
+    for dy in range(-erode, erode + 1):
+        for dx in range(-erode, erode + 1):
+            sh = np.full_like(lab, -2)
+            ys = slice(max(0, dy), height + min(0, dy))
+            yd = slice(max(0, -dy), height + min(0, -dy))
+            xs = slice(max(0, dx), width + min(0, dx))
+            xd = slice(max(0, -dx), width + min(0, -dx))
+            sh[yd, xd] = lab[ys, xs]
+            keep &= sh == lab
+    return {nm: keep & (lab == i) for i, nm in enumerate(names)}
+
+
+def scene0_regions(camera, width, height, erode=3):
+    """{name: bool[H, W]} for scene 0's three fixed spheres: the first of them on the
+    pixel-centre ray, hit above y = SCENE0_SMALL_TOP + 0.1 (the camera looks down from
+    y = 2, so such a ray never crossed the random small spheres' layer first), every pixel
+    within `erode` pixels the same (defocus blur and jitter see both sides of an edge)."""
+    o, d = camera_rays(camera, width, height)
+    names = list(SCENE0_SPHERES)
+    T = np.stack([_sphere_t(o, d, c, r) for c, r in SCENE0_SPHERES.values()])
+    first = np.argmin(T, axis=0)
+    tbest = np.min(T, axis=0)
+    ok = np.isfinite(tbest) & (o[1] + tbest * d[..., 1] > SCENE0_SMALL_TOP + 0.1)
+    lab = np.where(ok, first, -1)
     keep = lab >= 0
     for dy in range(-erode, erode + 1):
         for dx in range(-erode, erode + 1):

@@ -14,6 +14,8 @@ Scenes 0 and 8 also carry fixed geometry whose pixels can be compared (masks
 from tests/gallery_regions.py, the same code the tests use):
   * scene 0: the open sky above the horizon, whose bytes are exact: the packed
     mask of pixels equal to the sky colour (217, 230, 255) over rows 0-135;
+  * scene 0: the three fixed spheres' means of the linearised bytes (pixels whose ray
+    meets them above the random small spheres' layer);
   * scene 8: per deterministic region (light quad, glass / metal / blue-fog /
     earth / Perlin spheres) the pixel count and the mean of the linearised
     bytes ((b/255)^2.2, the inverse of Texture.saveAsPNG's gamma), and the
@@ -66,6 +68,13 @@ def main():
                          "width": int(g0.shape[1]),
                          "full_rows": int(next(r for r in range(SKY_ROWS) if not sky[r].all())),
                          "mask_packbits_b64": base64.b64encode(np.packbits(sky.reshape(-1)).tobytes()).decode()}
+    # scene 0: the three fixed spheres (linearised byte means)
+    lin0 = (g0.astype(np.float64) / 255.0) ** 2.2
+    h0, w0 = g0.shape[:2]
+    regs0 = gr.scene0_regions(rtamd.Scene(0, w0, h0, seed=1).camera, w0, h0)
+    out["scene0_regions"] = {"source": "galleries/book1_final(scene0).png", "width": w0, "height": h0,
+                             "regions": {k: {"n_pixels": int(m.sum()), "lin_mean": np.round(lin0[m].mean(0), 6).tolist()}
+                                         for k, m in regs0.items()}}
     # scene 8: deterministic regions (linearised byte means) and the earth's block pattern
     g8 = np.asarray(Image.open(os.path.join(GALLERY, "book2_final(scene8).png")).convert("RGB")).astype(np.float64)
     lin = (g8 / 255.0) ** 2.2
