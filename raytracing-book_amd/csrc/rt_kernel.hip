@@ -577,7 +577,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
 // otherwise the NaN-ignoring min/max form.  The choice is wave-uniform and made
 // once per walk, outside the loop (3.6 % faster on scene 8 than testing it per
 // node step).  Reading both successors while the node is tested (to hide the
-// dependent LDS read) measured 9 % slower: the node loop is issue-bound.
+// dependent LDS read) measured 9 % slower: its extra VALU outweigh the hidden latency.
 // Node reads: an LDS address is the node's byte offset plus the dynamic region's
 // base, which is 0 in a kernel without static LDS (every non-stats build), so
 // the offset is the address itself (no add per step).
