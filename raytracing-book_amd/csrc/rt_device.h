@@ -35,9 +35,9 @@
 // slots (RT_LDS_ACC_BYTES), all in the dynamic region (no static LDS)
 #define RT_LDS_ACC_BYTES (512 * 16)
 #define RT_LDS_DYN_BYTES (80 * 1024 - RT_LDS_ACC_BYTES)   // link nodes + Perlin + media, or variant 61's tree + stacks
-// the pooled link-walk kernel as one 1024-thread workgroup per CU (16 waves, 4 per SIMD as
-// two of 512): one copy of the nodes per CU leaves room for the leaf tests' sphere and box
-// records; 8 KB of the 160 KB stay for the stats build's static counters
+// the pooled link-walk kernel as one 1024-thread workgroup per CU (16 waves, 4 per SIMD, the
+// same as two workgroups of 512): one copy of the nodes per CU leaves room for the leaf
+// tests' sphere and box records; 8 KB of the 160 KB stay for the stats build's static counters
 #define RT_LDS_BIG_BYTES (152 * 1024)
 #define RT_LDS_NODE_BYTES (64 * 1024)   // threaded (meta-word) nodes in LDS when they fit
 
