@@ -615,13 +615,13 @@ __device__ __forceinline__ uint32_t link_walk(const char* __restrict__ base, uin
 // link_walk for a wave's walking lanes that stops once `need` of them hold a hit
 // leaf or have ended (the others keep their position nx >= 0 and go on in the
 // next round): the wave does not step its last walkers alone while the lanes
-// waiting at a leaf idle.  Checked every second step.
+// waiting at a leaf idle.  Checked every third step (every second: scene 6 +2.7%, scenes 0 / 8 +0.6..0.8%).
 template <bool EXACT, bool STATS>
 __device__ __forceinline__ uint32_t link_walk_part(const char* __restrict__ base, uint32_t nx, v3 o, v3 inv,
                                                    float tmin, float tmax, int need, unsigned long long* st) {
     for (;;) {
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < 3; k++) {
             if ((int)nx >= 0) {
                 if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
                 float4 n0, n1;
