@@ -41,6 +41,8 @@ enum {
 #define RT_MAX_TEXTURES 8        /* uniform sampler2D textures[8], compute.glsl:23 */
 #define RT_MAX_RECORDS 65535     /* 16-bit indices in packed ids (App. C)          */
 #define RT_MAX_BVH_DEPTH 64      /* int stack[64], compute.glsl:229                */
+#define RT_MAX_IMAGE_DIM 65536   /* image width / height (pixel coordinates feed rand()) */
+#define RT_MAX_RAND_FACTOR 1024.0f /* |u_rand_factor| (see rt_render)                */
 
 typedef struct rt_ctx rt_ctx;
 
@@ -77,13 +79,15 @@ int rt_set_camera(rt_ctx* ctx, const float ubo[28]);
 int rt_set_params(rt_ctx* ctx, int max_depth, const float background[3],
                   float sqrt_spp, float recip_sqrt_spp);
 
-/* (Re)allocate the RGBA32F accumulation image, zero-filled.
+/* (Re)allocate the RGBA32F accumulation image, zero-filled; 1 <= w, h <= RT_MAX_IMAGE_DIM.
  * Replaces: Texture.resize on the framebuffer callback (Window.java:116-129). */
 int rt_resize(rt_ctx* ctx, int w, int h);
 
 /* Run n_frames progressive frames.  Equal to n_frames x { frame_count =
  * first_frame+i; u_rand_factor = rand_factors[i]; glDispatchCompute;
- * glMemoryBarrier }.  Asynchronous on the context's stream(s).
+ * glMemoryBarrier }.  Asynchronous on the context's stream(s).  Each rand
+ * factor must be finite with |value| <= RT_MAX_RAND_FACTOR (the reference
+ * passes (float)Math.random() in [0, 1); beyond, rand()'s +0.001 steps vanish).
  * Replaces: RaytraceExecutor.raytrace (RaytraceExecutor.java:100-142). */
 int rt_render(rt_ctx* ctx, int first_frame, int n_frames, const float* rand_factors);
 

@@ -30,21 +30,72 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
                          unsigned int* info_out, size_t info_cap, int* slots_out, int* n_slots);
 
 /* Host-only: the link-format copy of a reference BVH upload that the default
- * kernel stages in LDS (rt_device.h RT_LINK_*): per threaded node two float4
- * (box, hit / miss successor byte offsets), then the leaves' (types, prims)
- * as uint2.  *n_f4 = its float4 count, 0 when the BVH has too many nodes for
- * 16-bit offsets (the kernel then walks the threaded nodes). */
+ * kernel walks (rt_device.h RT_LINK_*): the threaded nodes placed breadth-first,
+ * two float4 each (box, hit / miss successor byte addresses), then the leaves'
+ * (types | next address << 8, prims) as uint2.  *n_f4 = its float4 count, 0 when
+ * there is no BVH. */
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4);
+
+/* Host-only: the boxes' 48-byte records rt_upload_buffer(RT_BIND_BOXES) builds
+ * (rt_capi.hip box_record: 3 float4 per box; float4[2].y = 1 for a compact record,
+ * whose faces the kernel rebuilds from it) and how many are compact. */
+int rt_debug_box_records(const void* boxes, size_t nbytes, void* out, size_t out_cap, int* n_compact);
 
 /* Diagnostic build of the render kernel with wave-level region timers and
  * active-lane counters (never used for timed numbers).  enable=1 switches the
- * context to it and zeroes the counters; read returns n <= 64 counters. */
+ * context to it and zeroes the counters; read returns n <= 64 counters.
+ * The stats kernels exist only in the A/B build (librtamd_ab.so, built with
+ * -DRT_AB_KNOBS); the release library returns RT_ERR_STATE. */
 struct rt_ctx;
 int rt_debug_enable_stats(struct rt_ctx* ctx, int enable);
 int rt_debug_read_stats(struct rt_ctx* ctx, unsigned long long* out, int n);
 
 /* Number of visible HIP devices (0 when none). */
 int rt_debug_device_count(void);
+
+/* 1 when this library is the A/B build (-DRT_AB_KNOBS: kernel variants, stats
+ * twins, non-exact ablations and the RT_* environment knobs), 0 for the release
+ * library, whose output depends on nothing but its inputs. */
+int rt_debug_ab_build(void);
+
+/* Per-context options for tests and A/B runs, set by explicit calls (never read
+ * from the environment by the release library).  Every option below 100 changes
+ * only how the work is laid out or which exact form of a test runs, never a bit
+ * of the image (tests/ compare each against the default).  Options >= 100 exist
+ * in the A/B build only (the release library returns RT_ERR_INVALID_ARG). */
+enum {
+    RT_OPTION_BOX_PRETEST = 1,          /* box bounds pre-test (1)                          */
+    RT_OPTION_FASTDIV = 2,              /* shared-reciprocal division where exact (1)       */
+    RT_OPTION_SPH_LDS = 3,              /* leaf records staged in LDS (1)                   */
+    RT_OPTION_BIG_WG = 4,               /* 1024-thread workgroups when records fit (1)      */
+    RT_OPTION_CHUNK_TARGET = 5,         /* ordered units per resident wave; 0 = one per tile (16) */
+    RT_OPTION_STAGED_CHUNK_TARGET = 6,  /* staged units per resident wave (48)              */
+    RT_OPTION_STAGE_TILES = 7,          /* stage chunks below this many tiles per wave (2^20) */
+    RT_OPTION_SM_BATCH = 8,             /* shading batch, lanes (64)                        */
+    RT_OPTION_SM_FRAC = 9,              /* shading batch, 64ths of the walking lanes (56)   */
+    RT_OPTION_WALK_FRAC = 10,           /* partial node walks, 64ths (48)                   */
+    RT_OPTION_WATCHDOG_MS = 11,         /* a wave that stores no sample for this long sets
+                                           the fault word and leaves (120000); 0 = at once  */
+    RT_OPTION_CHUNK_WAIT_MS = 12,       /* ordered-chunk wait bound (30000); 0 = at once    */
+    RT_OPTION_LDS_NODE_CAP = 13,        /* bytes of BVH nodes staged in LDS; the rest is
+                                           read from global memory (0 = as many as fit)     */
+    RT_OPTION_COMPACT_BOXES = 14,       /* canonical boxes from 48-byte LDS records (1)     */
+    RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
+    RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
+};
+int rt_debug_set_option(struct rt_ctx* ctx, int option, int value);
+int rt_debug_get_option(struct rt_ctx* ctx, int option, int* value);
+
+/* What the last rt_render launched on the context's first device (tests assert
+ * that the intended path ran):
+ *   out[0] launch shape (0 fast-lds, 1 fast-global, 2 link-lds, 3 meta-lds,
+ *          4 meta-global, 5 link two-level: top nodes in LDS, the rest global)
+ *   out[1] workgroup size          out[2] shared-reciprocal division on (1/0)
+ *   out[3] box pre-test on (1/0)   out[4] dynamic LDS bytes
+ *   out[5] BVH nodes staged in LDS out[6] box records: bit 0 compact tests, bit 1 in LDS
+ *   out[7] staged chunks (1/0)     out[8] chunks per launch
+ * n <= 16 ints are written; returns RT_ERR_STATE before the first render. */
+int rt_debug_last_launch(struct rt_ctx* ctx, int* out, int n);
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,43 @@ int rts_get_camera(const rts_scene* s, float ubo[28]);
 /* Re-aim the camera for a new image size (Scene.updateCamera). */
 int rts_set_image_size(rts_scene* s, int width, int height);
 
+/* ---- Custom scenes: the reference's builder calls one by one (Scene.java's
+ * statements).  rts_new starts an empty world (RaytraceModel's and the texture
+ * classes' static lists); textures and materials are objects the models share,
+ * as in Java; rts_finish runs RaytraceModel.putModelsToProgram (BVH build and
+ * packers), Solid/CheckerTexture.putDataToTexture and Camera.init, after which
+ * the rts_get_* calls return the scene's bytes.  Handles are >= 0 ints; every
+ * call returns 0 or a negative rt.h error code (message: rts_last_error). */
+int rts_new(uint64_t seed, const char* asset_dir, rts_scene** out);
+/* SolidTexture.registerColor / CheckerTexture(c1, c2, scale) / new PerlinNoiseTexture(scale)
+ * / ImageTexture.create(asset, shift): *tex = the packed texture id (Texture.getValue). */
+int rts_solid_texture(rts_scene* s, float r, float g, float b, int* tex);
+int rts_checker_texture(rts_scene* s, const float c1[3], const float c2[3], float scale, int* tex);
+int rts_perlin_texture(rts_scene* s, float scale, int* tex);
+int rts_image_texture(rts_scene* s, const char* asset_name, int shift_x, int shift_y, int* tex);
+/* new Lambertian(tex) / Metal(tex, fuzz = param) / Dielectric(ior = param) /
+ * DiffuseLight(emit) / Isotropic(tex); kind = RT_MAT_*. */
+int rts_material(rts_scene* s, int kind, int texture, float param, const float emit[3], int* material);
+/* new Sphere(center1[, center2], r, mat) / Quad(q, u, v, mat) / Box(a, b, mat) or
+ * Box(a, b, translation, rotation in radians, mat) / ConstantMedium(boundary, density, mat):
+ * *model = the model's handle (not yet in the world). */
+int rts_sphere(rts_scene* s, const float center1[3], const float center2[3], float radius, int material, int* model);
+int rts_quad(rts_scene* s, const float q[3], const float u[3], const float v[3], int material, int* model);
+int rts_box(rts_scene* s, const float a[3], const float b[3], const float translation[3], const float rotation[3],
+            int material, int* model);
+int rts_constant_medium(rts_scene* s, int boundary_model, float density, int material, int* model);
+/* RaytraceModel.addModel / addLight (RaytraceModel.java:57-79). */
+int rts_add_model(rts_scene* s, int model);
+int rts_add_light(rts_scene* s, int model);
+/* Camera.lookFrom/lookAt/vup/vfov/defocusAngle/focusDist and the background colour. */
+typedef struct rts_camera_params {
+    float look_from[3], look_at[3], vup[3];
+    float vfov, defocus_angle, focus_dist;
+    float background[3];
+} rts_camera_params;
+int rts_camera(rts_scene* s, const rts_camera_params* p);
+int rts_finish(rts_scene* s, int width, int height);
+
 /* RaytraceExecutor.setSamplePerPixel: sqrt_spp = (float)Math.sqrt(spp). */
 void rts_spp_uniforms(int spp, float* sqrt_spp, float* recip_sqrt_spp);
 

@@ -76,7 +76,7 @@ def _fp(a):
 class OracleScene:
     """Keeps the scene bytes alive and describes them to the oracle."""
 
-    def __init__(self, scene, max_depth=5, spp=1, background=None):
+    def __init__(self, scene, max_depth=5, spp=1, background=None, uniforms=None):
         from rtamd.scene import spp_uniforms   # host-side uniform helper
         self.keep = []
         d = OracleSceneDesc()
@@ -98,7 +98,8 @@ class OracleScene:
         bg = scene.background if background is None else background
         for i in range(3):
             d.background[i] = float(bg[i])
-        d.sqrt_spp, d.recip_sqrt_spp = spp_uniforms(spp)
+        d.sqrt_spp, d.recip_sqrt_spp = spp_uniforms(spp) if uniforms is None else (float(uniforms[0]),
+                                                                                   float(uniforms[1]))
         self.desc = d
         self.width, self.height = scene.width, scene.height
 

@@ -37,6 +37,7 @@ struct Device {
     bool timed = false;
     DevBuf nodes, spheres, quads, boxes, media, lights, tex[8];
     DevBuf dquads, dboxes;   // intersection-only face records (rt_device.h)
+    DevBuf dboxc;            // compact canonical box records (RT_BOXC_F4 per box)
     DevBuf image;            // internal image
     DevBuf args;             // rt_kernel_args slot in device memory
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
@@ -128,7 +129,14 @@ struct rt_ctx {
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
     bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
     bool sph_lds = true;   // sphere records' first two float4 in LDS when they fit (env RT_SPH_LDS=0 disables; A/B)
-    size_t sample_budget = (size_t)32 << 30;
+    bool compact_boxes = true;   // boxes' compact records when every box has one (box_test_compact; option 0: A/B)
+    int lds_node_cap = 0;        // bytes of BVH nodes staged in LDS, 0 = as many as fit (tests: force the two-level walk)
+    int n_boxc_ok = 0;           // boxes whose compact record reproduces their faces
+    unsigned long long watchdog_ticks = 120ull * 100000000ull;     // render_stream progress bound (100 MHz ticks)
+    unsigned long long chunk_wait_ticks = 30ull * 100000000ull;    // ordered-chunk wait bound
+    size_t sample_budget = (size_t)32 << 30;   // staged colours per launch, at most (and at most half the free memory)
+    int last_launch[RT_LI_N] = {0};
+    bool launched = false;
 };
 
 namespace {
@@ -293,18 +301,38 @@ bool boxes_nest(const std::vector<rt_dnode>& dn) {
     return true;
 }
 
-// The threaded BVH in link format (rt_device.h RT_LINK_*; variant 37's node
-// loop, rt_kernel.hip trace): node k is (xmin, xmax, ymin, ymax), (zmin, zmax,
-// hit successor, miss successor) at byte offset 32 k; an inner node's hit
-// successor is node k + 1, a leaf's leaves the loop with its leaf ordinal and
-// skip offset; the leaves' (types, prims) follow the nodes as uint2.  Same
-// node sequence as the threaded walk.  Empty when the offsets do not fit.
+// The threaded BVH in link format (rt_device.h RT_LINK_*; rt_kernel.hip link_walk):
+// the same nodes and boxes, placed breadth-first (node k's children in the threaded
+// array are its right child k + 1 and its left child skip(k + 1)), each with its
+// successor addresses: on a box hit an inner node continues at its right child (the
+// reference pushes left then right and pops right first, compute.glsl:259-260), a leaf
+// leaves the loop with its ordinal; on a miss both continue at the threaded skip node.
+// Leaf j's record follows the nodes: (prim types | the skip node's address << 8,
+// prims), in threaded order.  The walk therefore visits the threaded walk's node
+// sequence (tests/test_link_nodes.py), and the top levels every ray walks sit at the
+// lowest addresses, the part a two-level launch stages in LDS.  Empty when there is
+// no BVH or it has more nodes than 16-bit indices address.
 std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
     std::vector<float4> out;
     const size_t n = dn.size();
+    if (n == 0 || n > RT_LINK_MAX_NODES) return out;
+    auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
+    std::vector<uint32_t> pos(n, 0xFFFFFFFFu), order;
+    order.reserve(n);
+    order.push_back(0);
+    for (size_t h = 0; h < order.size(); h++) {
+        const uint32_t k = order[h];
+        if (pos[k] != 0xFFFFFFFFu || order.size() > n) return std::vector<float4>();
+        pos[k] = (uint32_t)h;
+        if (is_leaf(k)) continue;
+        const uint32_t l = k + 1 < n ? (dn[k + 1].meta & 0xFFFFu) : RT_NODE_END;
+        if (k + 1 >= n || l == RT_NODE_END || l >= n) return std::vector<float4>();
+        order.push_back(k + 1);
+        order.push_back(l);
+    }
+    if (order.size() != n) return out;
     size_t nl = 0;
-    for (const rt_dnode& d : dn) nl += (d.meta & 0xF0000u) != 0;
-    if (n == 0 || n > RT_LINK_MAX_NODES || nl > 0x7FFF) return out;
+    for (size_t k = 0; k < n; k++) nl += is_leaf(k);
     out.assign(2 * n + (nl + 1) / 2, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     uint2* leaves = reinterpret_cast<uint2*>(out.data() + 2 * n);
     auto f = [](uint32_t u) {
@@ -316,14 +344,18 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
     for (size_t k = 0; k < n; k++) {
         const rt_dnode& d = dn[k];
         const uint32_t skip = d.meta & 0xFFFFu;
-        const uint32_t miss = skip == RT_NODE_END ? RT_LINK_END : 32u * skip;
-        uint32_t hit = 32u * (uint32_t)(k + 1);
-        if ((d.meta & 0xF0000u) != 0) {
-            hit = RT_LINK_LEAF | li << 16 | (skip == RT_NODE_END ? 0xFFFFu : 32u * skip);
-            leaves[li++] = make_uint2(d.meta & 0xFF0000u, d.prims);
+        const uint32_t skip_at = skip == RT_NODE_END ? RT_LINK_END : 32u * pos[skip];
+        uint32_t hit;
+        if (is_leaf(k)) {
+            hit = RT_LINK_LEAF | li;
+            const uint32_t next = skip == RT_NODE_END ? RT_LINK_NEXT_END : skip_at;
+            leaves[li++] = make_uint2(((d.meta >> 16) & 0xFFu) | next << 8, d.prims);
+        } else {
+            hit = 32u * pos[k + 1];
         }
-        out[2 * k] = make_float4(d.xmin, d.xmax, d.ymin, d.ymax);
-        out[2 * k + 1] = make_float4(d.zmin, d.zmax, f(hit), f(miss));
+        const uint32_t at = pos[k];
+        out[2 * at] = make_float4(d.xmin, d.xmax, d.ymin, d.ymax);
+        out[2 * at + 1] = make_float4(d.zmin, d.zmax, f(hit), f(skip_at));
     }
     return out;
 }
@@ -628,6 +660,84 @@ void face_record(const rt_quad& q, float4 out[3]) {
     out[2] = make_float4(v[a], v[b], delta, csf);
 }
 
+// The compact record of a box with Box.java's axis-aligned layout (rt_kernel.hip
+// box_test_compact, rt_device.h RT_BOXC_F4): its corners mn / mx as its faces' q carry
+// them (Box.java:32-37) and its faces' normal components along z, x, y.  The kernel
+// rebuilds every value its canonical test reads from these with the operations below;
+// the record is kept (out[2].y = 1) only when each rebuilt value equals the one the
+// uploaded faces give (face_record, the canonical planes), else the box takes the
+// full record path.  Float equality: the sign of a zero is the one freedom, and no
+// result depends on it (box_test_compact).
+bool compact_box(const rt_quad* Q, float4 out[3]) {
+    const float mnx = Q[0].q[0], mny = Q[0].q[1], mxz = Q[0].q[2], mxx = Q[1].q[0], mnz = Q[2].q[2],
+                mxy = Q[4].q[1];
+    const float sz = Q[0].normal[2], sx = Q[1].normal[0], sy = Q[4].normal[1];
+    out[0] = make_float4(mnx, mny, mnz, mxx);
+    out[1] = make_float4(mxy, mxz, sz, sx);
+    out[2] = make_float4(sy, 0.0f, 0.0f, 0.0f);
+    static const int kAx[6] = {2, 0, 2, 0, 1, 1};   // Box.java:32-37 face order: normals along z, x, z, x, y, y
+    const float sv[6] = {sz, sx, -sz, -sx, sy, -sy};
+    const float qk[6] = {mxz, mxx, mnz, mnx, mxy, mny};
+    const float DX = mxx - mnx, DY = mxy - mny, DZ = mxz - mnz;
+    auto cs = [](int c) {
+        float x;
+        std::memcpy(&x, &c, 4);
+        return x;
+    };
+    // box_test_compact's per-face systems (boxc_face)
+    const float4 A[6] = {make_float4(mnx, mny, DX, 0.0f), make_float4(mny, mxz, 0.0f, -DZ),
+                         make_float4(mxx, mny, -DX, 0.0f), make_float4(mny, mnz, 0.0f, DZ),
+                         make_float4(mnx, mxz, DX, 0.0f), make_float4(mnx, mnz, DX, 0.0f)};
+    const float4 B[6] = {make_float4(0.0f, DY, DX * DY, cs(0)), make_float4(DY, 0.0f, DZ * DY, cs(2)),
+                         make_float4(0.0f, DY, -(DX * DY), cs(0)), make_float4(DY, 0.0f, -(DZ * DY), cs(2)),
+                         make_float4(0.0f, -DZ, -(DX * DZ), cs(1)), make_float4(0.0f, DZ, DX * DZ, cs(1))};
+    auto same = [](float4 a, float4 b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; };
+    for (int i = 0; i < 6; i++) {
+        const rt_quad& q = Q[i];
+        const int ax = kAx[i];
+        for (int k = 0; k < 3; k++)
+            if (!std::isfinite(q.normal[k]) || !std::isfinite(q.q[k]) || !std::isfinite(q.u[k]) || !std::isfinite(q.v[k]))
+                return false;
+        // the canonical plane: normal (s_i along its axis, zeros elsewhere), d = s_i * q_k
+        if (q.normal[ax] != sv[i] || sv[i] == 0.0f || q.normal[(ax + 1) % 3] != 0.0f || q.normal[(ax + 2) % 3] != 0.0f)
+            return false;
+        if (q.d != sv[i] * qk[i]) return false;
+        float4 f[3];
+        face_record(q, f);
+        uint32_t c0, c1;
+        std::memcpy(&c0, &f[2].w, 4);
+        std::memcpy(&c1, &B[i].w, 4);
+        if (!same(f[1], A[i]) || f[2].x != B[i].x || f[2].y != B[i].y || f[2].z != B[i].z || c0 != c1) return false;
+    }
+    out[2].y = 1.0f;
+    return true;
+}
+
+// A box's bounds (dboxes[21..22]): min / max over its faces' corners, rounded to float.
+void box_bounds(const rt_quad* Q, float4 out[2]) {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < 6; i++)
+        for (int k = 0; k < 3; k++)
+            for (int cu = 0; cu < 2; cu++)
+                for (int cv = 0; cv < 2; cv++) {
+                    const double x = (double)Q[i].q[k] + cu * (double)Q[i].u[k] + cv * (double)Q[i].v[k];
+                    lo[k] = std::min(lo[k], x);
+                    hi[k] = std::max(hi[k], x);
+                }
+    out[0] = make_float4((float)lo[0], (float)hi[0], (float)lo[1], (float)hi[1]);
+    out[1] = make_float4((float)lo[2], (float)hi[2], 0.0f, 0.0f);
+}
+
+// A box's 48-byte record (rt_kernel.hip leaf_prims_t): compact (compact_box) or, when its
+// faces cannot be rebuilt from one, just its bounds (dboxes[21..22]) for the pre-test.
+bool box_record(const rt_quad* Q, const float4 bounds[2], float4 rb[RT_BOXC_F4]) {
+    if (compact_box(Q, rb)) return true;
+    rb[0] = make_float4(bounds[0].x, bounds[0].z, bounds[1].x, bounds[0].y);
+    rb[1] = make_float4(bounds[0].w, bounds[1].y, 0.0f, 0.0f);
+    rb[2] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    return false;
+}
+
 // The scene side of the shared-reciprocal division regime (rt_kernel.hip rcp_nr /
 // div_nr): coordinates within 2^20 (so are the rays' origins and directions: hit
 // points, camera rays, scatter and light-sampling directions), a face's delta
@@ -756,6 +866,9 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (n_devices <= 0 || n_devices > 64 || (!device_ids && n_devices > count))
         return fail(RT_ERR_INVALID_ARG, "rt_create: bad device count");
     rt_ctx* c = new rt_ctx();
+#ifdef RT_AB_KNOBS
+    // A/B build only: the structure variants and knobs from the environment (tools/ab_variants.py).
+    // The release library reads no environment: its output depends on its inputs alone.
     if (const char* v = std::getenv("RT_KERNEL_VARIANT")) {
         // 0 (default), 37, 30, 61 and their stats twins 39, 38, 31, 69
         // (rt_kernel.hip rt_launch_render); anything else is the default
@@ -774,7 +887,10 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_WALK_FRAC")) c->walk_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SPH_LDS")) c->sph_lds = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_BIG_WG")) c->big_wg = std::atoi(v) != 0;
+    if (const char* v = std::getenv("RT_COMPACT_BOXES")) c->compact_boxes = std::atoi(v) != 0;
+    if (const char* v = std::getenv("RT_LDS_NODE_CAP")) c->lds_node_cap = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("RT_DEBUG_FLAGS")) c->debug_flags = std::atoi(v);
+#endif
     c->devs.resize(n_devices);
     for (int i = 0; i < n_devices; i++) {
         Device& d = c->devs[i];
@@ -801,7 +917,7 @@ int rt_destroy(rt_ctx* c) {
         dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter);
         dev_free(d.tile_done); dev_free(d.samples); dev_free(d.wbuf); dev_free(d.dquads); dev_free(d.dboxes);
-        dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links);
+        dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links); dev_free(d.dboxc);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
             if (e) (void)hipEventDestroy(e);
@@ -850,6 +966,8 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
         c->dnodes.swap(dn);
     }
     std::vector<float4> faces;   // intersection-only copy of quads / box sides
+    std::vector<float4> boxc;    // compact canonical box records
+    int n_cmp = 0;
     if (binding == RT_BIND_QUADS || binding == RT_BIND_BOXES) {
         const rt_quad* qs = (const rt_quad*)bytes;
         size_t nq = nbytes / sizeof(rt_quad);   // a box is 6 consecutive quads
@@ -865,36 +983,25 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
             // planes (RT_DBOX_F4 float4)
             c->boxes_canon = true;
             c->boxes_cond = true;
+            boxc.assign((nq / 6) * RT_BOXC_F4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
             for (size_t bx = 0; bx < nq / 6; bx++) {
                 float4* o = &faces[bx * RT_DBOX_F4];
                 float sw[12];
-                double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-                for (int i = 0; i < 6; i++) {   // the bounds: every face's corners
+                for (int i = 0; i < 6; i++) {
                     const rt_quad& Q = qs[bx * 6 + i];
                     // the face test solves alpha, beta on the reference's axis pair (face_record);
                     // |delta| >= half of |u_a v_b| + |u_b v_a| bounds how far a point it accepts
                     // can lie outside the face (a few ulps of the scene's extent)
-                    {
-                        const float* u = Q.u;
-                        const float* v = Q.v;
-                        int ka = 1, kb = 2;
-                        if (u[0] * v[1] - u[1] * v[0] != 0.0f) { ka = 0; kb = 1; }
-                        else if (u[0] * v[2] - u[2] * v[0] != 0.0f) { ka = 0; kb = 2; }
-                        const double t1 = (double)u[ka] * v[kb], t2 = (double)u[kb] * v[ka];
-                        if (!(std::fabs(t1 - t2) >= 0.5 * (std::fabs(t1) + std::fabs(t2))) || t1 == t2)
-                            c->boxes_cond = false;
-                    }
-                    for (int k = 0; k < 3; k++) {
-                        for (int cu = 0; cu < 2; cu++)
-                            for (int cv = 0; cv < 2; cv++) {
-                                const double x = (double)Q.q[k] + cu * (double)Q.u[k] + cv * (double)Q.v[k];
-                                lo[k] = std::min(lo[k], x);
-                                hi[k] = std::max(hi[k], x);
-                            }
-                    }
+                    const float* u = Q.u;
+                    const float* v = Q.v;
+                    int ka = 1, kb = 2;
+                    if (u[0] * v[1] - u[1] * v[0] != 0.0f) { ka = 0; kb = 1; }
+                    else if (u[0] * v[2] - u[2] * v[0] != 0.0f) { ka = 0; kb = 2; }
+                    const double t1 = (double)u[ka] * v[kb], t2 = (double)u[kb] * v[ka];
+                    if (!(std::fabs(t1 - t2) >= 0.5 * (std::fabs(t1) + std::fabs(t2))) || t1 == t2)
+                        c->boxes_cond = false;
                 }
-                o[21] = make_float4((float)lo[0], (float)hi[0], (float)lo[1], (float)hi[1]);
-                o[22] = make_float4((float)lo[2], (float)hi[2], 0.0f, 0.0f);
+                box_bounds(qs + bx * 6, o + 21);
                 for (int i = 0; i < 6; i++) {
                     float4 f[3];
                     face_record(qs[bx * 6 + i], f);
@@ -913,11 +1020,13 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
                 o[18] = make_float4(sw[0], sw[1], sw[2], sw[3]);
                 o[19] = make_float4(sw[4], sw[5], sw[6], sw[7]);
                 o[20] = make_float4(sw[8], sw[9], sw[10], sw[11]);
+                n_cmp += box_record(qs + bx * 6, o + 21, &boxc[bx * RT_BOXC_F4]);
                 // the canonical test shares one reciprocal per axis: opposite faces' normals negated
                 if (sw[4] != -sw[0] || sw[6] != -sw[2] || sw[10] != -sw[8]) fd = false;
             }
         }
         c->fd_ok[binding] = fd;
+        if (binding == RT_BIND_BOXES) c->n_boxc_ok = n_cmp;
     }
     if (binding == RT_BIND_SPHERES) {
         const rt_sphere* sp = (const rt_sphere*)bytes;
@@ -948,6 +1057,10 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
         if (binding == RT_BIND_QUADS || binding == RT_BIND_BOXES) {
             r = dev_alloc_copy(c, d, binding == RT_BIND_QUADS ? d.dquads : d.dboxes, faces.data(),
                                faces.size() * sizeof(float4));
+            if (r) return r;
+        }
+        if (binding == RT_BIND_BOXES) {
+            r = dev_alloc_copy(c, d, d.dboxc, boxc.data(), boxc.size() * sizeof(float4));
             if (r) return r;
         }
     }
@@ -1025,7 +1138,8 @@ int rt_padded_local_rows(int height, int world, int stripe_rows) {
 
 int rt_resize(rt_ctx* c, int w, int h) {
     if (!c) return RT_ERR_INVALID_ARG;
-    if (w <= 0 || h <= 0 || (size_t)w * h > ((size_t)1 << 30)) return set_err(c, RT_ERR_INVALID_ARG, "bad image size");
+    if (w <= 0 || h <= 0 || w > RT_MAX_IMAGE_DIM || h > RT_MAX_IMAGE_DIM || (size_t)w * h > ((size_t)1 << 30))
+        return set_err(c, RT_ERR_INVALID_ARG, "bad image size");
     c->width = w;
     c->height = h;
     for (Device& d : c->devs) {
@@ -1077,11 +1191,20 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     if (c->width <= 0) return set_err(c, RT_ERR_STATE, "rt_resize before rt_render");
     if (!c->have_cam) return set_err(c, RT_ERR_STATE, "rt_set_camera before rt_render");
     if (!c->uploaded[RT_BIND_BVH]) return set_err(c, RT_ERR_STATE, "no BVH uploaded");
+    // u_rand_factor is (float)Math.random() in the reference (RaytraceExecutor.java:124-127).
+    // rand() adds 0.001 to it per call (random.glsl:2-7): a NaN / inf, or a value so large
+    // that the addition no longer changes it, would freeze rand() and keep a rejection
+    // loop (random.glsl:19-24, 40-45) spinning on the device forever
+    for (int i = 0; i < n_frames; i++)
+        if (!(std::fabs(rand_factors[i]) <= RT_MAX_RAND_FACTOR))
+            return set_err(c, RT_ERR_INVALID_ARG, "rand_factors must be finite with |value| <= 1024");
     int r = validate(c);
     if (r) return r;
     rt_kernel_args a;
     std::memset(&a, 0, sizeof(a));
     a.n_nodes = c->n_dnodes;
+    a.watchdog_ticks = c->watchdog_ticks;
+    a.chunk_wait_ticks = c->chunk_wait_ticks;
     int32_t lc = 0;
     if (c->host_buf[RT_BIND_LIGHTS].size() >= 4) std::memcpy(&lc, c->host_buf[RT_BIND_LIGHTS].data(), 4);
     a.lights_count = lc;
@@ -1120,67 +1243,87 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
     a.debug_flags = c->debug_flags;
     a.n_lnode_f4 = (int)c->links.size();
-    // Perlin table in LDS after the nodes (default launch shapes only; rt_kernel.hip texture_color);
-    // variant 37 stages the link-format nodes (and may use 80 KB)
+    // LDS plan of the link-format shapes (rt_kernel.hip rt_launch_render): from address 0 the
+    // nodes, then the leaf records, the Perlin table (6 x 256 R32F), the media records with
+    // their sphere boundaries, the spheres' intersection halves (A, B) and the canonical
+    // boxes' compact records -- each when it fits.  512-thread workgroups (2 per CU,
+    // RT_LDS_DYN_BYTES each) when everything fits them, else one of 1024 threads per CU
+    // (RT_LDS_BIG_BYTES); when not even the nodes and leaves fit that, the two-level walk:
+    // the top levels (breadth-first prefix) in LDS, the rest of the nodes and the leaf
+    // records in global memory.  The A/B structures 37 (one pixel per lane: 512 threads,
+    // the lanes' running means after what is staged) and 61 (its own tree) plan below too.
     const bool fast_walk = c->variant == 61 || c->variant == 69;
-    const bool links = !fast_walk && c->variant != 30 && c->variant != 31 && a.n_lnode_f4 > 0;
-    const bool shape_p = !fast_walk;
-    const size_t node_f4 = links ? (size_t)a.n_lnode_f4 : (size_t)2 * c->n_dnodes;
-    size_t lds_cap = links ? RT_LDS_DYN_BYTES : RT_LDS_NODE_BYTES;
-    // The pooled link-walk kernel (variant 0 / 39) runs as one 1024-thread workgroup per CU
-    // when everything below (with the spheres' and the canonical boxes' leaf-test records)
-    // fits RT_LDS_BIG_BYTES and some of it would not fit the 512-thread shape.
-    const bool pooled_link = links && (c->variant == 0 || c->variant == 39);
+    const bool pooled = c->variant == 0 || c->variant == 39;
     const int n_sph = (int)(c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere));
     const int n_box = (int)(c->host_buf[RT_BIND_BOXES].size() / sizeof(rt_box));
     const int n_med = (int)(c->host_buf[RT_BIND_MEDIA].size() / sizeof(rt_medium));
-    a.block = 512;
-    if (pooled_link && c->big_wg) {
-        size_t perlin_f4 = 0;
-        for (int t = 0; t < RT_MAX_TEXTURES; t++)
-            if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) {
-                perlin_f4 = (size_t)c->tex_w[t] * c->tex_h[t] / 4;
-                break;
-            }
-        const size_t box_f4 = (c->boxes_canon && c->sph_lds) ? 5 * (size_t)n_box : 0;
-        const size_t all_f4 = node_f4 + perlin_f4 + (n_med <= 64 ? 3 * (size_t)n_med : 0) +
-                              (c->sph_lds ? 2 * (size_t)n_sph : 0) + box_f4;
-        if (all_f4 * 16 <= RT_LDS_BIG_BYTES && all_f4 * 16 > RT_LDS_DYN_BYTES) {
-            a.block = 1024;
-            lds_cap = RT_LDS_BIG_BYTES;
-        }
-    }
-    a.perlin_slot = a.perlin_lds = -1;
-    for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
-        if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
-    if (a.perlin_slot >= 0 && shape_p &&
-        node_f4 * 16 + (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] * 4 <= lds_cap)
-        a.perlin_lds = (int)node_f4;
-    // media records (+ sphere boundary) after it, for the same shapes (3 float4 per medium)
-    a.n_media = (int)(c->host_buf[RT_BIND_MEDIA].size() / sizeof(rt_medium));
-    a.media_lds = -1;
-    {
-        const size_t base = node_f4 +
-                            (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] / 4 : 0);
-        if (a.n_media > 0 && a.n_media <= 64 && shape_p && (base + 3 * (size_t)a.n_media) * 16 <= lds_cap)
-            a.media_lds = (int)base;
-    }
-    // the spheres' (A, B) after them, for the pooled link-walk kernel (variant 0 / 39): the leaf
-    // tests' sphere loads become LDS reads when the whole set fits the shape's budget; then,
-    // in the 1024-thread shape, the canonical boxes' bounds and planes
-    a.sph_lds = a.box_lds = -1;
+    a.n_media = n_med;
     a.n_sph_lds = n_sph;
     a.n_box_lds = n_box;
+    a.box_all_cmp = (c->compact_boxes && n_box > 0 && c->n_boxc_ok == n_box) ? 1 : 0;
+    a.perlin_slot = -1;
+    for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
+        if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
     {
-        size_t base = (a.media_lds >= 0) ? (size_t)a.media_lds + 3 * (size_t)a.n_media
-                      : node_f4 + (a.perlin_lds >= 0 ? (size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] / 4
-                                                     : 0);
-        if (c->sph_lds && pooled_link && n_sph > 0 && (base + 2 * (size_t)n_sph) * 16 <= lds_cap) {
-            a.sph_lds = (int)base;
-            base += 2 * (size_t)n_sph;
+        const size_t node_f4 = 2 * (size_t)c->n_dnodes;
+        const size_t leaf_f4 = (size_t)a.n_lnode_f4 > node_f4 ? (size_t)a.n_lnode_f4 - node_f4 : 0;
+        const size_t perlin_f4 =
+            a.perlin_slot >= 0 ? ((size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] + 3) / 4 : 0;
+        const size_t media_f4 = (n_med > 0 && n_med <= 64) ? 3 * (size_t)n_med : 0;
+        const size_t sph_f4 = (c->sph_lds && pooled) ? 2 * (size_t)n_sph : 0;
+        const size_t box_f4 = (size_t)RT_BOXC_F4 * n_box;   // every box's record (bounds; compact faces)
+        const size_t cap_s = RT_LDS_DYN_BYTES / 16, cap_b = RT_LDS_BIG_BYTES / 16;
+        const size_t ess = node_f4 + leaf_f4 + perlin_f4 + media_f4;   // what every walk and shade reads
+        const size_t all = ess + sph_f4 + box_f4;
+        const size_t node_cap = c->lds_node_cap > 0 ? (size_t)c->lds_node_cap / 32 * 2 : node_f4;
+        const bool big_ok = c->big_wg && pooled;
+        // A/B: threaded meta-word nodes (variant 30, or 37 when the link nodes do not fit 512 threads)
+        const bool meta = !fast_walk && !pooled && (c->variant == 30 || c->variant == 31 || ess > cap_s);
+        size_t cap;
+        bool tl = false;
+        if (fast_walk) {
+            cap = 0;   // variant 61 stages its own tree (rt_launch_render)
+        } else if (meta) {
+            cap = cap_s;
+        } else if (node_cap < node_f4 && pooled) {
+            tl = true;
+            cap = cap_b;
+        } else if (all <= cap_s || (ess <= cap_s && !(big_ok && all <= cap_b))) {
+            cap = cap_s;
+        } else if (big_ok && ess <= cap_b) {
+            cap = cap_b;
+        } else {
+            tl = pooled;
+            cap = tl ? cap_b : cap_s;
         }
-        if (a.block == 1024 && c->boxes_canon && c->sph_lds && n_box > 0 && (base + 5 * (size_t)n_box) * 16 <= lds_cap)
-            a.box_lds = (int)base;
+        a.block = cap == cap_b ? 1024 : 512;
+        size_t at = 0;
+        a.lds_node_f4 = 0;
+        a.leaf_lds = -1;
+        a.perlin_lds = a.media_lds = a.sph_lds = a.box_cmp_lds = -1;
+        if (meta) {
+            at = node_f4;   // the threaded nodes (32 B each) from address 0 (rt_launch_render: META_LDS)
+        } else if (!fast_walk && a.n_lnode_f4 > 0) {
+            if (tl) {
+                // the top levels after the small tables the shading reads (placed below)
+                const size_t room = cap - perlin_f4 - media_f4;
+                a.lds_node_f4 = (int)(std::min(std::min(node_f4, node_cap), room) & ~(size_t)1);
+                at = (size_t)a.lds_node_f4;
+            } else {
+                a.lds_node_f4 = (int)node_f4;
+                a.leaf_lds = (int)node_f4;
+                at = node_f4 + leaf_f4;
+            }
+        }
+        if (!fast_walk) {
+            if (perlin_f4 && at + perlin_f4 <= cap) { a.perlin_lds = (int)at; at += perlin_f4; }
+            if (media_f4 && at + media_f4 <= cap) { a.media_lds = (int)at; at += media_f4; }
+            if (!tl) {
+                if (sph_f4 && at + sph_f4 <= cap) { a.sph_lds = (int)at; at += sph_f4; }
+                if (box_f4 && at + box_f4 <= cap) { a.box_cmp_lds = (int)at; at += box_f4; }
+            }
+        }
+        a.lds_end_f4 = (int)at;
     }
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
@@ -1199,6 +1342,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         a.boxes = (const rt_box*)d.boxes.ptr;
         a.dquads = (const float4*)d.dquads.ptr;
         a.dboxes = (const float4*)d.dboxes.ptr;
+        a.dboxc = (const float4*)d.dboxc.ptr;
         a.media = (const rt_medium*)d.media.ptr;
         a.lights = (const int32_t*)d.lights.ptr;
         for (int t = 0; t < 8; t++) {
@@ -1250,8 +1394,16 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         const bool staged = chunks_wanted > 1 && few_tiles;
         const size_t n_pixels = (size_t)d.local_rows * c->width;
         if (staged) {
+            // staged colours per launch: at most sample_budget and half the device's free memory
+            // (what this context already holds counts as free), and at most 2^31 samples (the
+            // kernel's 32-bit sample index)
+            size_t budget = c->sample_budget;
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, (free_b + d.samples.bytes) / 2);
             const size_t per_frame = n_pixels * sizeof(float4);
-            per_launch = (int)std::max<size_t>(1, std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, c->sample_budget / per_frame));
+            size_t frames = std::min<size_t>(RT_MAX_FRAMES_PER_LAUNCH, budget / per_frame);
+            frames = std::min<size_t>(frames, ((size_t)1 << 31) / std::max<size_t>(n_pixels, 1));
+            per_launch = (int)std::max<size_t>(1, frames);
         }
         {   // equal launches: no short last launch that the whole grid waits on
             const int n_launch = (std::max(n_frames, 1) + per_launch - 1) / per_launch;
@@ -1302,13 +1454,15 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             int slot = d.ring_pos++ % Device::kRing;
             HIPCHK(c, hipEventSynchronize(d.ring_ev[slot]));   // the copy that last used this slot is done
             d.ring[slot] = a;
-            if (rt_launch_render(d.ring[slot], (rt_kernel_args*)d.args.ptr, d.stream))
+            if (rt_launch_render(d.ring[slot], (rt_kernel_args*)d.args.ptr, d.stream,
+                                 &d == &c->devs[0] ? c->last_launch : nullptr))
                 return set_err(c, RT_ERR_DEVICE, std::string("kernel launch failed: ") +
                                                      hipGetErrorString(hipGetLastError()));
             HIPCHK(c, hipEventRecord(d.ring_ev[slot], d.stream));
         }
         HIPCHK(c, hipEventRecord(d.ev_stop, d.stream));
         d.timed = true;
+        c->launched = c->launched || n_frames > 0;
     }
     (void)max_ns;
     return RT_OK;
@@ -1324,7 +1478,7 @@ int rt_sync(rt_ctx* c) {
             HIPCHK(c, hipMemcpy(&fault, (unsigned*)d.counter.ptr + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
             if (fault) {
                 HIPCHK(c, hipMemset((unsigned*)d.counter.ptr + 1, 0, sizeof(unsigned)));
-                return set_err(c, RT_ERR_DEVICE, fault == 2 ? "render kernel: a wave exceeded its time bound"
+                return set_err(c, RT_ERR_DEVICE, fault == 2 ? "render kernel: a wave stored no sample within its progress bound (watchdog)"
                                                             : "render kernel: ordered-chunk wait timed out");
             }
         }
@@ -1453,6 +1607,24 @@ int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t ou
     return RT_OK;
 }
 
+int rt_debug_box_records(const void* boxes, size_t nbytes, void* out, size_t out_cap, int* n_compact) {
+    if (!boxes || !n_compact || nbytes % sizeof(rt_box)) return RT_ERR_INVALID_ARG;
+    const size_t nb = nbytes / sizeof(rt_box);
+    if (out && out_cap < nb * RT_BOXC_F4 * sizeof(float4)) return RT_ERR_INVALID_ARG;
+    // the upload's own path (rt_upload_buffer(RT_BIND_BOXES))
+    std::vector<float4> recs(nb * RT_BOXC_F4);
+    int n = 0;
+    const rt_quad* qs = (const rt_quad*)boxes;
+    for (size_t bx = 0; bx < nb; bx++) {
+        float4 b[2];
+        box_bounds(qs + 6 * bx, b);
+        n += box_record(qs + 6 * bx, b, &recs[bx * RT_BOXC_F4]);
+    }
+    *n_compact = n;
+    if (out) std::memcpy(out, recs.data(), recs.size() * sizeof(float4));
+    return RT_OK;
+}
+
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4) {
     if (!bvh || !n_f4 || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
     std::vector<rt_dnode> dn;
@@ -1510,6 +1682,9 @@ static int stats_twin(int v) {
 
 int rt_debug_enable_stats(rt_ctx* c, int on) {
     if (!c) return RT_ERR_INVALID_ARG;
+#ifndef RT_AB_KNOBS
+    if (on) return set_err(c, RT_ERR_STATE, "the stats kernels are in the A/B build (librtamd_ab.so)");
+#endif
     for (Device& d : c->devs) {
         HIPCHK(c, hipSetDevice(d.id));
         HIPCHK(c, hipStreamSynchronize(d.stream));
@@ -1541,6 +1716,77 @@ int rt_debug_read_stats(rt_ctx* c, unsigned long long* out, int n) {
         if (r) return r;
         for (int i = 0; i < n; i++) out[i] += tmp[i];
     }
+    return RT_OK;
+}
+
+int rt_debug_ab_build(void) {
+#ifdef RT_AB_KNOBS
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+int rt_debug_set_option(rt_ctx* c, int option, int v) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    auto bad = [&]() { return set_err(c, RT_ERR_INVALID_ARG, "option value out of range"); };
+    switch (option) {
+        case RT_OPTION_BOX_PRETEST: c->box_pretest = v != 0; break;
+        case RT_OPTION_FASTDIV: c->fastdiv = v != 0; break;
+        case RT_OPTION_SPH_LDS: c->sph_lds = v != 0; break;
+        case RT_OPTION_BIG_WG: c->big_wg = v != 0; break;
+        case RT_OPTION_COMPACT_BOXES: c->compact_boxes = v != 0; break;
+        case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
+        case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
+        case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
+        case RT_OPTION_SM_BATCH: if (v < 1 || v > 64) return bad(); c->sm_batch = v; break;
+        case RT_OPTION_SM_FRAC: if (v < 1 || v > 64) return bad(); c->sm_frac = v; break;
+        case RT_OPTION_WALK_FRAC: if (v < 1 || v > 64) return bad(); c->walk_frac = v; break;
+        case RT_OPTION_WATCHDOG_MS: if (v < 0) return bad(); c->watchdog_ticks = (unsigned long long)v * 100000ull; break;
+        case RT_OPTION_CHUNK_WAIT_MS: if (v < 0) return bad(); c->chunk_wait_ticks = (unsigned long long)v * 100000ull; break;
+        case RT_OPTION_LDS_NODE_CAP: if (v < 0) return bad(); c->lds_node_cap = v; break;
+#ifdef RT_AB_KNOBS
+        case RT_OPTION_KERNEL_VARIANT:
+            if (!(v == 0 || v == 30 || v == 31 || v == 37 || v == 38 || v == 39 || v == 61 || v == 69)) return bad();
+            c->variant = v;
+            break;
+        case RT_OPTION_DEBUG_FLAGS: c->debug_flags = v; break;
+#endif
+        default: return set_err(c, RT_ERR_INVALID_ARG, "unknown option (A/B options need librtamd_ab.so)");
+    }
+    return RT_OK;
+}
+
+int rt_debug_get_option(rt_ctx* c, int option, int* v) {
+    if (!c || !v) return RT_ERR_INVALID_ARG;
+    switch (option) {
+        case RT_OPTION_BOX_PRETEST: *v = c->box_pretest; break;
+        case RT_OPTION_FASTDIV: *v = c->fastdiv; break;
+        case RT_OPTION_SPH_LDS: *v = c->sph_lds; break;
+        case RT_OPTION_BIG_WG: *v = c->big_wg; break;
+        case RT_OPTION_COMPACT_BOXES: *v = c->compact_boxes; break;
+        case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
+        case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
+        case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;
+        case RT_OPTION_SM_BATCH: *v = c->sm_batch; break;
+        case RT_OPTION_SM_FRAC: *v = c->sm_frac; break;
+        case RT_OPTION_WALK_FRAC: *v = c->walk_frac; break;
+        case RT_OPTION_WATCHDOG_MS: *v = (int)std::min<unsigned long long>(INT_MAX, c->watchdog_ticks / 100000ull); break;
+        case RT_OPTION_CHUNK_WAIT_MS: *v = (int)std::min<unsigned long long>(INT_MAX, c->chunk_wait_ticks / 100000ull); break;
+        case RT_OPTION_LDS_NODE_CAP: *v = c->lds_node_cap; break;
+#ifdef RT_AB_KNOBS
+        case RT_OPTION_KERNEL_VARIANT: *v = c->variant; break;
+        case RT_OPTION_DEBUG_FLAGS: *v = c->debug_flags; break;
+#endif
+        default: return set_err(c, RT_ERR_INVALID_ARG, "unknown option (A/B options need librtamd_ab.so)");
+    }
+    return RT_OK;
+}
+
+int rt_debug_last_launch(rt_ctx* c, int* out, int n) {
+    if (!c || !out || n < 0 || n > RT_LI_N) return RT_ERR_INVALID_ARG;
+    if (!c->launched) return set_err(c, RT_ERR_STATE, "no render launched yet");
+    std::memcpy(out, c->last_launch, sizeof(int) * (size_t)n);
     return RT_OK;
 }
 

@@ -30,6 +30,7 @@
 #define RT_NODE_END 0xFFFFu
 #define RT_DFACE_F4 3    // float4 per dquads record
 #define RT_DBOX_F4 23    // float4 per dboxes record
+#define RT_BOXC_F4 3     // float4 per compact box record (canonical boxes, box_test_compact)
 // LDS per 512-thread workgroup (2 workgroups per CU share 160 KiB): what the
 // launch shape stages (at most RT_LDS_DYN_BYTES), then the lanes' running-mean
 // slots (RT_LDS_ACC_BYTES), all in the dynamic region (no static LDS)
@@ -54,14 +55,21 @@ struct rt_dnode {
 };
 static_assert(sizeof(rt_dnode) == 32, "device node is 32 B");
 
-// Link format of the same nodes (variant 37): word 6 / 7 of a node are the
-// successors on a box hit / miss as byte offsets into the node array, so the
+// Link format of the same nodes (the default walk): word 6 / 7 of a node are the
+// successors on a box hit / miss as byte addresses into the node array, so the
 // node loop is one select.  A hit leaf's successor leaves the loop:
-// RT_LINK_LEAF | leaf << 16 | the skip offset (0xFFFF = end of walk); the end
-// of the walk is RT_LINK_END.  Both have the sign bit set.
+// RT_LINK_LEAF | leaf ordinal; the end of the walk is RT_LINK_END (both have the
+// sign bit set).  Leaf j's record (uint2, after the nodes) is (types | next << 8,
+// prims): the prim types in bits 0-7 (left, right), then the address the walk
+// continues at after the leaf's tests (its skip node; RT_LINK_NEXT_END = end).
+// Nodes are placed breadth-first (the root's level first): when the whole array
+// does not fit LDS, the first lds_node_f4 / 2 nodes -- the top levels every ray
+// walks -- are staged in LDS and an address at or past them reads global memory
+// (the two-level walk).  Up to 65535 nodes (the reference's 16-bit indices).
 #define RT_LINK_LEAF 0x80000000u
 #define RT_LINK_END 0xFFFFFFFFu
-#define RT_LINK_MAX_NODES 2047   // offsets (32 B per node) fit 16 bits below 0xFFFF
+#define RT_LINK_NEXT_END 0xFFFFFFu
+#define RT_LINK_MAX_NODES 65535
 
 struct rt_dtex {
     const void* data;   // RGBA8 (uint32) or R32F
@@ -77,6 +85,7 @@ struct rt_kernel_args {
     const rt_box* boxes;
     const float4* dquads;
     const float4* dboxes;
+    const float4* dboxc;         // per box RT_BOXC_F4 float4: the compact record (box_test_compact)
     const rt_medium* media;
     const int32_t* lights;
     int n_nodes, lights_count;
@@ -121,8 +130,7 @@ struct rt_kernel_args {
                                  // per medium, after the Perlin table), or -1
     int sph_lds;                 // float4 offset of the spheres' intersection halves (A, B) in LDS, or -1
     int n_sph_lds;               // spheres staged there
-    int box_lds;                 // float4 offset of the canonical boxes' bounds + planes (5 float4 each) in LDS, or -1
-    int n_box_lds;               // boxes staged there
+    int n_box_lds;               // boxes whose compact records are staged (all of them)
     int block;                   // the render kernel's workgroup size: 512, or 1024 (one per CU) when the
                                  // records above fit its LDS (RT_LDS_BIG_BYTES)
     int acc_lds;                 // float4 offset of the lanes' running-mean slots (after everything staged)
@@ -139,13 +147,30 @@ struct rt_kernel_args {
     const uint2* f2leaves;       // (meta, prims) per leaf
     int n_f2inner, n_f2leaves, f2depth;
     // the reference's threaded BVH with explicit successors (variant 0/37; rt_capi.hip build_links)
-    const float4* lnodes;        // 2 float4 per node, then the leaves' (types, prims) as uint2
-    int n_lnode_f4;              // float4 of the whole array; 0 = not available (too many nodes)
+    const float4* lnodes;        // 2 float4 per node, then the leaves' (types | next << 8, prims) as uint2
+    int n_lnode_f4;              // float4 of the whole array; 0 = not available (no BVH)
+    int lds_node_f4;             // float4 of nodes staged in LDS (from address 0): all 2 * n_nodes, or
+                                 // the top levels (two-level walk: addresses past them read lnodes)
+    int leaf_lds;                // float4 offset of the leaf records in LDS, or -1 (read from lnodes)
+    int lds_end_f4;              // float4 end of everything the link-format shapes stage in LDS
+    int box_cmp_lds;             // float4 offset of the boxes' 48-byte records in LDS (RT_BOXC_F4 each), or
+                                 // -1 (read from dboxc)
+    int box_all_cmp;             // every box's record is compact (box_test_compact); else the full box test
+    // bounds of the device-side waits, in ticks of the 100 MHz real-time clock (s_memrealtime)
+    unsigned long long watchdog_ticks;     // render_stream: no sample stored by the wave for this long
+                                           // -> fault word 2, the wave leaves (checked on its first pass
+                                           // and every 256th; 0 = at the first check)
+    unsigned long long chunk_wait_ticks;   // ordered chunks: wait for the previous chunk -> fault word 1
     float rand_factors[RT_MAX_FRAMES_PER_LAUNCH];
 };
 
+// What rt_launch_render launched (rt_debug_last_launch)
+enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
+       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_N = 16 };
+
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)
-int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream);   // sets a.acc_lds
+// sets a.acc_lds; info (may be NULL): RT_LI_* of the launch
+int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int* info);
 // debug: evaluate GLSL built-ins on device (tests)
 int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream);

@@ -26,6 +26,7 @@
 // rand() consumption order is identical to the reference.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -41,6 +42,8 @@ typedef rt_kernel_args KP;
 #define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_stream)
 #define RT_OPT_FD 4     // with RT_OPT_SM: the scene is in the shared-reciprocal division regime (P.fastdiv)
 #define RT_OPT_STREAM 8 // with RT_OPT_SM: the wave streams over units (render_stream) instead of one at a time
+#define RT_OPT_TL 16    // with RT_OPT_STREAM: two-level walk (top levels in LDS, the rest of the nodes global)
+#define RT_OPT_BOXC 32  // with RT_OPT_STREAM: every box has a compact record (box_test_compact), no full box test
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -274,66 +277,68 @@ __device__ __forceinline__ bool box_test(const float4* __restrict__ fb, v3 o, v3
     return has;
 }
 
-// box_test for a box with Box.java's axis-aligned layout (P.boxes_canon): face i's
-// normal is s_i along axis z, x, z, x, y, y, so for finite o and d
-// dot(n, d) = s_i*d_k and dot(n, o) = s_i*o_k exactly (the other products are
-// exact zeros; a zero sign differs only where the face is skipped or t is 0 <
-// tmin).  The planes come from the record's compact tail (fb[18..20]).
-// fd (P.fastdiv also guarantees s_2 = -s_0, s_3 = -s_1, s_5 = -s_4): each axis'
-// pair of faces divides by +-(s * d_k), so one reciprocal per axis, negated for the
-// opposite face; a plane t is kept only when >= tmin = 0.001, never in the
-// tiny-numerator case.
-// c0..c2: the record's canonical planes (fb[18..20], from global memory or LDS).
-__device__ __forceinline__ bool box_test_canon_c(float4 c0, float4 c1, float4 c2, const float4* __restrict__ fb, v3 o,
-                                                 v3 d, float tmin, float tmax, float& t, int& face, float& alpha,
-                                                 float& beta, bool fd = false) {
-    const float sv[6] = {c0.x, c0.z, c1.x, c1.z, c2.x, c2.z};
-    const float wv[6] = {c0.y, c0.w, c1.y, c1.w, c2.y, c2.w};
-    const float dk[6] = {d.z, d.x, d.z, d.x, d.y, d.y};
-    const float ok[6] = {o.z, o.x, o.z, o.x, o.y, o.y};
-    float ti[6];
-    unsigned cand = 0;
-    if (fd) {
-        // by axis: faces (0, 2), (1, 3), (4, 5)
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const int i = k == 2 ? 4 : k, j = k == 2 ? 5 : k + 2;
-            const float den_i = sv[i] * dk[i], den_j = sv[j] * dk[j];
-            const float r = rcp_nr(den_i);
-            ti[i] = div_nr(wv[i] - sv[i] * ok[i], den_i, r);   // unused when |denom| < 1e-8
-            ti[j] = div_nr(wv[j] - sv[j] * ok[j], den_j, -r);
-            if (!(fabsf(den_i) < 1e-8f) && (tmin <= ti[i] && ti[i] <= tmax)) cand |= 1u << i;
-            if (!(fabsf(den_j) < 1e-8f) && (tmin <= ti[j] && ti[j] <= tmax)) cand |= 1u << j;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            const float denom = sv[i] * dk[i];
-            ti[i] = (wv[i] - sv[i] * ok[i]) / denom;   // unused when |denom| < 1e-8
-            if (!(fabsf(denom) < 1e-8f) && (tmin <= ti[i] && ti[i] <= tmax)) cand |= 1u << i;
-        }
-    }
-    bool has = false;
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        if ((cand >> i) & 1u) {
-            float al, be;
-            if (ti[i] <= tmax && face_interior(ldg(fb + 6 + 2 * i), ldg(fb + 7 + 2 * i), o, d, ti[i], al, be, fd)) {
-                tmax = ti[i];
-                t = ti[i];
-                face = i;
-                alpha = al;
-                beta = be;
-                has = true;
-            }
-        }
-    }
-    return has;
+// The canonical box test from a compact record (RT_BOXC_F4 float4, rt_capi.hip compact_box):
+// c0 = (mn.x, mn.y, mn.z, mx.x), c1 = (mx.y, mx.z, s_z, s_x), c2 = (s_y, ok, 0, 0) -- the box's
+// corners (Box.java:19-37 builds its six faces from them) and its faces' normal components.
+// Everything the face tests read is rebuilt with the builder's own float operations:
+// the edges DX = mx.x - mn.x (Box.java's dx, dy, dz), the planes (s_i, s_i * q_k) with the
+// opposite faces' normals negated, and each face's 2-D system (A, B) on the reference's axis
+// pair with its delta.  The host rebuilds the same values with the same operations and keeps
+// a box's record (ok = 1) only when they equal the uploaded faces' records (float equality:
+// a zero's sign is the only freedom, and it cannot reach a result: it only makes a zero
+// plane numerator, alpha or beta a zero of the other sign, which every test and the uv's
+// texture lookup treat alike).  So the test reads 48 B of LDS instead of 80 B of LDS plus up
+// to 192 B of face systems from global memory.
+template <int I>
+__device__ __forceinline__ void boxc_face(float mnx, float mny, float mnz, float mxx, float mxz, float DX, float DY,
+                                          float DZ, float4& A, float4& B) {
+    // faces of Box.java:32-37: q, u, v of side I (face_record's axis pair and delta expression)
+    if (I == 0) { A = make_float4(mnx, mny, DX, 0.0f); B = make_float4(0.0f, DY, DX * DY, __int_as_float(0)); }
+    if (I == 1) { A = make_float4(mny, mxz, 0.0f, -DZ); B = make_float4(DY, 0.0f, DZ * DY, __int_as_float(2)); }
+    if (I == 2) { A = make_float4(mxx, mny, -DX, 0.0f); B = make_float4(0.0f, DY, -(DX * DY), __int_as_float(0)); }
+    if (I == 3) { A = make_float4(mny, mnz, 0.0f, DZ); B = make_float4(DY, 0.0f, -(DZ * DY), __int_as_float(2)); }
+    if (I == 4) { A = make_float4(mnx, mxz, DX, 0.0f); B = make_float4(0.0f, -DZ, -(DX * DZ), __int_as_float(1)); }
+    if (I == 5) { A = make_float4(mnx, mnz, DX, 0.0f); B = make_float4(0.0f, DZ, DX * DZ, __int_as_float(1)); }
 }
-__device__ __forceinline__ bool box_test_canon(const float4* __restrict__ pl, const float4* __restrict__ fb, v3 o,
-                                               v3 d, float tmin, float tmax, float& t, int& face, float& alpha,
-                                               float& beta, bool fd = false) {
-    return box_test_canon_c(ldg(pl), ldg(pl + 1), ldg(pl + 2), fb, o, d, tmin, tmax, t, face, alpha, beta, fd);
+__device__ __forceinline__ bool box_test_compact(float4 c0, float4 c1, float4 c2, v3 o, v3 d, float tmin, float tmax,
+                                                 float& t, int& face, float& alpha, float& beta, bool fd = false) {
+    const float mnx = c0.x, mny = c0.y, mnz = c0.z, mxx = c0.w, mxy = c1.x, mxz = c1.y;
+    const float sz = c1.z, sx = c1.w, sy = c2.x;
+    // faces in the reference's order (hitting.glsl:135-146): each face's plane t, then its
+    // interior test when tmin <= t <= the current ray_t.max (fd: rcp_nr / div_nr per face;
+    // sharing one reciprocal per axis kept it live across the next faces' tests: more spills)
+    bool has = false;
+#define RT_BOXC_FACE(I, S, Q, DK, OK)                                                           \
+    {                                                                                                      \
+        const float s_ = (S), den = s_ * (DK);                                                             \
+        float ti;                                                                                          \
+        if (fd) {                                                                                          \
+            ti = div_nr(s_ * (Q) - s_ * (OK), den, rcp_nr(den));                                           \
+        } else {                                                                                           \
+            ti = (s_ * (Q) - s_ * (OK)) / den;                                                             \
+        }                                                                                                  \
+        if (!(fabsf(den) < 1e-8f) && (tmin <= ti && ti <= tmax)) {                                         \
+            float4 A, B;                                                                                   \
+            boxc_face<I>(mnx, mny, mnz, mxx, mxz, mxx - mnx, mxy - mny, mxz - mnz, A, B);                  \
+            float al, be;                                                                                  \
+            if (face_interior(A, B, o, d, ti, al, be, fd)) {                                               \
+                tmax = ti;                                                                                 \
+                t = ti;                                                                                    \
+                face = I;                                                                                  \
+                alpha = al;                                                                                \
+                beta = be;                                                                                 \
+                has = true;                                                                                \
+            }                                                                                              \
+        }                                                                                                  \
+    }
+    RT_BOXC_FACE(0, sz, mxz, d.z, o.z)
+    RT_BOXC_FACE(1, sx, mxx, d.x, o.x)
+    RT_BOXC_FACE(2, -sz, mnz, d.z, o.z)
+    RT_BOXC_FACE(3, -sx, mnx, d.x, o.x)
+    RT_BOXC_FACE(4, sy, mxy, d.y, o.y)
+    RT_BOXC_FACE(5, -sy, mny, d.y, o.y)
+#undef RT_BOXC_FACE
+    return has;
 }
 
 // hitting.glsl:148-160 for a medium boundary (only rec.t is read, :165-178).
@@ -493,7 +498,7 @@ __device__ __forceinline__ bool aabb_pk(float4 n0, float4 n1, v3 o, v3 inv, floa
 
 // The two prims of a leaf (compute.glsl:247-256), left then right.
 // FD: the shared-reciprocal divisions (rcp_nr / div_nr; FD kernels only).
-template <bool STATS, bool FD>
+template <bool STATS, bool FD, bool BOXC = false>
 __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, v3 inv, float a,
                                              float time, float tmin, float& tmax, float& rf, float px, float py, Hit& h,
                                              bool& has, unsigned long long* st) {
@@ -530,32 +535,37 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_QUAD_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_BOX) {
-            const float4* rec = P.dboxes + RT_DBOX_F4 * ix;
-            // LDS copy (P.box_lds >= 0, canonical boxes): bounds, then the canonical planes
-            const float4* lb = rt_dyn_lds + P.box_lds + 5 * ix;
+            // the box's 48-byte record (rt_capi.hip compact_box), from LDS when staged: its bounds
+            // for the pre-test, and -- every box of the scene having Box.java's axis-aligned
+            // layout (BOXC) -- everything its faces' tests read (box_test_compact); otherwise the
+            // faces' full records (box_test).  A canonical face is never hit by a ray with a
+            // non-finite origin or direction, in the reference's form or the compact one (its
+            // plane t or its alpha / beta is then inf or NaN), so BOXC needs no finiteness check.
+            float4 r0, r1, r2;
+            if (P.box_cmp_lds >= 0) {
+                const float4* cr = rt_dyn_lds + P.box_cmp_lds + RT_BOXC_F4 * ix;
+                r0 = cr[0];
+                r1 = cr[1];
+                r2 = cr[2];
+            } else {
+                const float4* cr = P.dboxc + RT_BOXC_F4 * ix;
+                r0 = ldg(cr);
+                r1 = ldg(cr + 1);
+                r2 = ldg(cr + 2);
+            }
             bool maybe = true;
-            if (P.box_margin > 0.0f && fin) {
+            if (P.box_margin > 0.0f && (BOXC || fin)) {
                 // the box's bounds grown by box_margin (rt_device.h): a ray that misses them
                 // misses every face the exact test below would accept
                 const float m = P.box_margin;
-                float4 b0, b1;
-                if (P.box_lds >= 0) {
-                    b0 = lb[0];
-                    b1 = lb[1];
-                } else {
-                    b0 = ldg(rec + 21);
-                    b1 = ldg(rec + 22);
-                }
-                maybe = aabb_pk(make_float4(b0.x - m, b0.y + m, b0.z - m, b0.w + m),
-                                make_float4(b1.x - m, b1.y + m, 0.0f, 0.0f), o, inv, tmin, tmax);
+                maybe = aabb_pk(make_float4(r0.x - m, r0.w + m, r0.y - m, r1.x + m),
+                                make_float4(r0.z - m, r1.y + m, 0.0f, 0.0f), o, inv, tmin, tmax);
             }
             if (maybe) {
-                if (P.boxes_canon && fin)
-                    hit = P.box_lds >= 0
-                              ? box_test_canon_c(lb[2], lb[3], lb[4], rec, o, d, tmin, tmax, t, face, al, be, fd)
-                              : box_test_canon(rec + 18, rec, o, d, tmin, tmax, t, face, al, be, fd);
+                if constexpr (BOXC)
+                    hit = box_test_compact(r0, r1, r2, o, d, tmin, tmax, t, face, al, be, fd);
                 else
-                    hit = box_test(rec, o, d, tmin, tmax, t, face, al, be, fd);
+                    hit = box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be, fd);
             }
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
@@ -582,21 +592,36 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
 // base, which is 0 in a kernel without static LDS (every non-stats build), so
 // the offset is the address itself (no add per step).
 typedef __attribute__((address_space(3))) const f4v lds_f4;
-template <bool EXACT, bool STATS>
-__device__ __forceinline__ uint32_t link_walk(const char* __restrict__ base, uint32_t nx, v3 o, v3 inv, float tmin,
-                                              float tmax, unsigned long long* st) {
+// Where the walk reads its nodes: LDS from `base` (the dynamic region) and, in the
+// two-level walk (TL), global memory `gnodes` for addresses at or past `lim`.
+struct NodeSrc {
+    const char* base;
+    const char* gnodes;
+    uint32_t lim;
+};
+template <bool STATS, bool TL>
+__device__ __forceinline__ void load_node(const NodeSrc& ns, uint32_t nx, float4& n0, float4& n1) {
+    if (TL && nx >= ns.lim) {   // below the LDS-staged top levels: the node array in global memory
+        const float4* g = reinterpret_cast<const float4*>(ns.gnodes + nx);
+        n0 = ldg(g);
+        n1 = ldg(g + 1);
+    } else if (STATS) {   // static LDS (the stats counters) precedes the dynamic region
+        n0 = *reinterpret_cast<const float4*>(ns.base + nx);
+        n1 = *reinterpret_cast<const float4*>(ns.base + nx + 16);
+    } else {
+        const lds_f4* p = (const lds_f4*)(uintptr_t)nx;
+        const f4v a = p[0], b = p[1];
+        n0 = make_float4(a.x, a.y, a.z, a.w);
+        n1 = make_float4(b.x, b.y, b.z, b.w);
+    }
+}
+template <bool EXACT, bool STATS, bool TL = false>
+__device__ __forceinline__ uint32_t link_walk(const NodeSrc& ns, uint32_t nx, v3 o, v3 inv, float tmin, float tmax,
+                                              unsigned long long* st) {
     while ((int)nx >= 0) {
         if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
         float4 n0, n1;
-        if (STATS) {   // static LDS (the stats counters) precedes the dynamic region
-            n0 = *reinterpret_cast<const float4*>(base + nx);
-            n1 = *reinterpret_cast<const float4*>(base + nx + 16);
-        } else {
-            const lds_f4* p = (const lds_f4*)(uintptr_t)nx;
-            const f4v a = p[0], b = p[1];
-            n0 = make_float4(a.x, a.y, a.z, a.w);
-            n1 = make_float4(b.x, b.y, b.z, b.w);
-        }
+        load_node<STATS, TL>(ns, nx, n0, n1);
         bool hit;
         if (!EXACT) {
             hit = aabb_pk(n0, n1, o, inv, tmin, tmax);
@@ -616,24 +641,16 @@ __device__ __forceinline__ uint32_t link_walk(const char* __restrict__ base, uin
 // leaf or have ended (the others keep their position nx >= 0 and go on in the
 // next round): the wave does not step its last walkers alone while the lanes
 // waiting at a leaf idle.  Checked every third step (every second: scene 6 +2.7%, scenes 0 / 8 +0.6..0.8%).
-template <bool EXACT, bool STATS>
-__device__ __forceinline__ uint32_t link_walk_part(const char* __restrict__ base, uint32_t nx, v3 o, v3 inv,
-                                                   float tmin, float tmax, int need, unsigned long long* st) {
+template <bool EXACT, bool STATS, bool TL = false>
+__device__ __forceinline__ uint32_t link_walk_part(const NodeSrc& ns, uint32_t nx, v3 o, v3 inv, float tmin,
+                                                   float tmax, int need, unsigned long long* st) {
     for (;;) {
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             if ((int)nx >= 0) {
                 if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
                 float4 n0, n1;
-                if (STATS) {
-                    n0 = *reinterpret_cast<const float4*>(base + nx);
-                    n1 = *reinterpret_cast<const float4*>(base + nx + 16);
-                } else {
-                    const lds_f4* p = (const lds_f4*)(uintptr_t)nx;
-                    const f4v a = p[0], b = p[1];
-                    n0 = make_float4(a.x, a.y, a.z, a.w);
-                    n1 = make_float4(b.x, b.y, b.z, b.w);
-                }
+                load_node<STATS, TL>(ns, nx, n0, n1);
                 bool hit;
                 if (!EXACT) {
                     hit = aabb_pk(n0, n1, o, inv, tmin, tmax);
@@ -675,24 +692,27 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
         // link-format nodes (rt_device.h RT_LINK_*): the successor is one select
         // between the node's hit and miss words; a hit leaf or the end leaves
         // the loop (sign bit)
-        const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
-        const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
+        NodeSrc ns;
+        ns.base = reinterpret_cast<const char*>(nodes);
+        ns.gnodes = nullptr;
+        ns.lim = 0;
+        const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + P.leaf_lds);
         uint32_t nx = 0u;
         if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);
         for (;;) {
             if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
             unsigned long long t0 = STATS ? clock64() : 0;
-            nx = wave_exact ? link_walk<true, STATS>(base, nx, o, inv, tmin, tmax, st)
-                            : link_walk<false, STATS>(base, nx, o, inv, tmin, tmax, st);
+            nx = wave_exact ? link_walk<true, STATS>(ns, nx, o, inv, tmin, tmax, st)
+                            : link_walk<false, STATS>(ns, nx, o, inv, tmin, tmax, st);
             if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
             if (nx == RT_LINK_END) break;
             unsigned long long t1 = STATS ? clock64() : 0;
             if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-            const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
-            leaf_prims_t<STATS, false>(P, lf.x, lf.y, o, d, inv, a, time, tmin, tmax, rf, px, py, h, has, st);
+            const uint2 lf = leaves[nx & 0x7FFFFFFFu];
+            leaf_prims_t<STATS, false>(P, lf.x << 16, lf.y, o, d, inv, a, time, tmin, tmax, rf, px, py, h, has, st);
             if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-            nx &= 0xFFFFu;
-            if (nx == 0xFFFFu) break;
+            nx = lf.x >> 8;
+            if (nx == RT_LINK_NEXT_END) break;
         }
         return has;
     }
@@ -853,7 +873,9 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_PERLIN) {    // :79-94
-        if (P.debug_flags & 1) return mk3s(0.5f);   // ablation only (RT_DEBUG_FLAGS), never exact
+#ifdef RT_AB_KNOBS
+        if (P.debug_flags & 1) return mk3s(0.5f);   // ablation only (A/B build, RT_DEBUG_FLAGS), never exact
+#endif
         float scale = ((float)detail_i / 4095.0f) * 100.0f;
         float accum = 0.0f, weight = 1.0f;
         const bool lds = P.perlin_lds >= 0 && (index & 7) == P.perlin_slot;
@@ -1097,9 +1119,7 @@ __device__ __forceinline__ int trace_fast(const KP& P, const float4* __restrict_
             else if (ty == RT_MODEL_QUAD)
                 hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, RT_INFINITY, t, al, be);
             else if (ty == RT_MODEL_BOX)
-                hit = P.boxes_canon ? box_test_canon(P.dboxes + RT_DBOX_F4 * ix + 18, P.dboxes + RT_DBOX_F4 * ix, o, d,
-                                                     tmin, RT_INFINITY, t, face, al, be)
-                                    : box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, RT_INFINITY, t, face, al, be);
+                hit = box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, RT_INFINITY, t, face, al, be);
             if (!hit) continue;
             if (t < best) {
                 second = best;
@@ -1601,8 +1621,8 @@ __device__ __forceinline__ void render_pool(const KP& P, const float4* __restric
 // one acquire fence, then plain loads.  The unit it waits for was dequeued
 // earlier by a running wave that waits only on earlier units, so the chain ends
 // at chunk 0; the poll is still bounded (RT_CHUNK_WAIT_TICKS of the 100 MHz
-// real-time clock) and a timeout sets P.fault, which rt_sync reports.
-#define RT_CHUNK_WAIT_TICKS 3000000000ull   // 30 s
+// real-time clock, P.chunk_wait_ticks: 30 s by default) and a timeout sets
+// P.fault, which rt_sync reports.
 typedef __attribute__((address_space(1))) unsigned gu32;   // global (never flat) accesses to shared words
 // tile and chunk are wave-uniform (readfirstlane): every lane polls / stores the
 // same word with the same value, so there is no lane-divergent control flow here
@@ -1612,7 +1632,7 @@ __device__ __forceinline__ void wait_chunk(const KP& P, int tile, int chunk) {
     while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
            (unsigned)chunk) {
         __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > RT_CHUNK_WAIT_TICKS) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= P.chunk_wait_ticks) {
             __hip_atomic_store((gu32*)P.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         }
@@ -1676,6 +1696,8 @@ __device__ __forceinline__ UnitGeo unit_geo(const KP& P, int u, int n_tiles, int
 template <bool STATS, int OPT, bool FD>
 __device__ __forceinline__ void render_stream(const KP& P, const float4* __restrict__ nodes, int gwave,
                                               unsigned long long* st) {
+    constexpr bool TL = (OPT & RT_OPT_TL) != 0;
+    constexpr bool BOXC = (OPT & RT_OPT_BOXC) != 0;
     const int lane = threadIdx.x & 63;
     const bool staged = P.samples != nullptr;
     const int tiles_x = (P.width + 7) >> 3;
@@ -1684,8 +1706,13 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     const uint32_t slot_f4 = 64u * (uint32_t)P.chunk_frames;
     float4* const wbase = staged ? nullptr : P.wbuf + (size_t)gwave * 2 * slot_f4;
     const rt_camera_ubo& C = P.cam;
-    const char* __restrict__ base = reinterpret_cast<const char*>(nodes);
-    const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + 2 * P.n_nodes);
+    NodeSrc ns;
+    ns.base = reinterpret_cast<const char*>(nodes);
+    ns.gnodes = reinterpret_cast<const char*>(P.lnodes);
+    ns.lim = (uint32_t)P.lds_node_f4 * 16u;
+    // the leaf records: LDS after the nodes, or (two-level) global memory after the node array
+    const uint2* __restrict__ leaves = TL ? reinterpret_cast<const uint2*>(P.lnodes + 2 * P.n_nodes)
+                                          : reinterpret_cast<const uint2*>(nodes + P.leaf_lds);
     const int batch = P.sm_batch;
     // wave-uniform: the units in the two slots (-1 = free) and their stored samples;
     // the pool: its unit, slot and next unclaimed sample
@@ -1706,14 +1733,24 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     v3 inv = mk3s(0.0f);
     uint32_t nx = RT_LINK_END;
     int status = RT_SM_FRESH;
-    // a bound on the wave's time (4x the chunk-wait bound): past it the wave sets the
-    // fault word (rt_sync reports it) and leaves, so a bug cannot keep the grid resident
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    // a progress watchdog: on its first pass and every 256th, a wave that has stored no
+    // sample since the previous check more than P.watchdog_ticks ago (120 s by default)
+    // sets the fault word (rt_sync reports it) and leaves, so a bug cannot keep the grid
+    // resident; a long launch that keeps storing samples never trips it
+    unsigned long long t_prog = __builtin_amdgcn_s_memrealtime();
+    uint32_t stored = 0, stored_seen = 0;   // wave-uniform: samples this wave stored
     uint32_t pass = 0;
     for (;;) {
-        if ((++pass & 255u) == 0 && __builtin_amdgcn_s_memrealtime() - t_start > 4 * RT_CHUNK_WAIT_TICKS) {
-            __hip_atomic_store((gu32*)P.fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
+        if ((pass++ & 255u) == 0) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (now - t_prog >= P.watchdog_ticks) {
+                __hip_atomic_store((gu32*)P.fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            if (stored != stored_seen) {
+                stored_seen = stored;
+                t_prog = now;
+            }
         }
         // fold the units whose samples are all stored, oldest first (ordered / one chunk)
         if (!staged) {
@@ -1856,12 +1893,12 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                 if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
                 unsigned long long t0 = STATS ? clock64() : 0;
                 if (P.walk_frac >= 64) {
-                    nx = wave_exact ? link_walk<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, st)
-                                    : link_walk<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, st);
+                    nx = wave_exact ? link_walk<true, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, st)
+                                    : link_walk<false, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, st);
                 } else {
                     const int needw = (__popcll(__ballot(1)) * P.walk_frac + 63) >> 6;
-                    nx = wave_exact ? link_walk_part<true, STATS>(base, nx, S.o, inv, 0.001f, tmax, needw, st)
-                                    : link_walk_part<false, STATS>(base, nx, S.o, inv, 0.001f, tmax, needw, st);
+                    nx = wave_exact ? link_walk_part<true, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, needw, st)
+                                    : link_walk_part<false, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, needw, st);
                 }
                 if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
                 if ((int)nx >= 0) {
@@ -1871,12 +1908,12 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                 } else {
                     unsigned long long t1 = STATS ? clock64() : 0;
                     if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-                    const uint2 lf = leaves[(nx >> 16) & 0x7FFFu];
-                    leaf_prims_t<STATS, FD>(P, lf.x, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf, fx, fy, h,
-                                            has, st);
+                    const uint2 lf = leaves[nx & 0x7FFFFFFFu];
+                    leaf_prims_t<STATS, FD, BOXC>(P, lf.x << 16, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf,
+                                                  fx, fy, h, has, st);
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-                    nx &= 0xFFFFu;
-                    if (nx == 0xFFFFu) status = RT_SM_HIT;
+                    nx = lf.x >> 8;   // the leaf's skip node
+                    if (nx == RT_LINK_NEXT_END) status = RT_SM_HIT;
                 }
             }
         }
@@ -1906,6 +1943,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
         const unsigned long long f_all = __ballot(fin), f_one = __ballot(fin && up == 1);
         done0 += (uint32_t)__popcll(f_all & ~f_one);
         done1 += (uint32_t)__popcll(f_one);
+        stored += (uint32_t)__popcll(f_all);
         // the end: no unit left to claim, every lane idle, every slot folded
         if (no_more && __ballot(status != RT_SM_FRESH) == 0 && (staged || (unit0 < 0 && unit1 < 0))) break;
     }
@@ -1958,9 +1996,14 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             fc.stack = reinterpret_cast<short*>(s_nodes) + tid;
         }
     } else if (LDSN) {
+        // link format: the nodes staged (all, or the two-level walk's top levels), then the leaf
+        // records when they are staged too; meta format: the threaded nodes
         const float4* g = LINK ? P.lnodes : reinterpret_cast<const float4*>(P.nodes);
-        const int nf4 = LINK ? P.n_lnode_f4 : 2 * P.n_nodes;
+        const int nf4 = LINK ? P.lds_node_f4 : 2 * P.n_nodes;
         for (int k = tid; k < nf4; k += BLOCK) s_nodes[k] = g[k];
+        if (LINK && P.leaf_lds >= 0)
+            for (int k = tid; k < P.n_lnode_f4 - 2 * P.n_nodes; k += BLOCK)
+                s_nodes[P.leaf_lds + k] = g[2 * P.n_nodes + k];
         if (P.perlin_lds >= 0) {   // the Perlin table after the nodes (host-sized launch)
             const rt_dtex& T = P.tex[P.perlin_slot];
             const float* src = reinterpret_cast<const float*>(T.data);
@@ -1983,12 +2026,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
             const float4* sp = reinterpret_cast<const float4*>(P.spheres);
             for (int k = tid; k < 2 * P.n_sph_lds; k += BLOCK) s_nodes[P.sph_lds + k] = ldg(sp + (k >> 1) * 3 + (k & 1));
         }
-        if (P.box_lds >= 0) {   // per canonical box: bounds (fb[21..22]), canonical planes (fb[18..20])
-            for (int k = tid; k < 5 * P.n_box_lds; k += BLOCK) {
-                const int b = k / 5, j = k - 5 * b;
-                s_nodes[P.box_lds + k] = ldg(P.dboxes + RT_DBOX_F4 * b + (j < 2 ? 21 + j : 16 + j));
-            }
-        }
+        if (P.box_cmp_lds >= 0)   // the boxes' compact records (box_test_compact)
+            for (int k = tid; k < RT_BOXC_F4 * P.n_box_lds; k += BLOCK) s_nodes[P.box_cmp_lds + k] = ldg(P.dboxc + k);
     }
     // per lane: the pixel's running mean during a unit, after what this launch
     // shape stages (P.acc_lds, set by rt_launch_render with the LDS size)
@@ -1999,7 +2038,7 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
     const int tiles_x = (P.width + 7) >> 3;
     const int n_tiles = tiles_x * ((P.local_rows + 7) >> 3);
     const int n_units = n_tiles * P.n_chunks;
-    if (LINK && !FAST && (OPT & RT_OPT_SM) && (OPT & RT_OPT_STREAM)) {
+    if constexpr (LINK && !FAST && (OPT & RT_OPT_SM) && (OPT & RT_OPT_STREAM)) {
         render_stream<STATS, OPT, (OPT & RT_OPT_FD) != 0>(P, rnodes, (int)blockIdx.x * (BLOCK / 64) + (tid >> 6), st);
     } else for (;;) {
         int unit = 0;
@@ -2133,63 +2172,62 @@ int rt_resident_waves(void) {
     return cus * 2 * (512 / 64);   // every shape: at most 2 workgroups of 512 per CU (launch_persistent)
 }
 
-int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
+int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int* info) {
     if (a.local_rows <= 0 || a.width <= 0 || a.n_frames <= 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    // Variants (RT_KERNEL_VARIANT; all bit-identical, tests/test_gpu_boundary.py):
-    //   0: pooled samples streamed over units with walks and shading in batches (render_stream)
-    //      over link-format nodes in LDS (+ the Perlin table and media records), 512 threads,
-    //      4 waves per SIMD; 39 its stats twin.  Falls back to pooled units one bounce at a
-    //      time (render_pool) over the threaded meta-word nodes (LDS, else global) when the
-    //      link format is unavailable (> 2047 nodes) or does not fit LDS.
-    //   37: the link walk with one pixel per lane (render_pixel, the round-1 default); 38 its
-    //      stats twin.
-    //   30: threaded nodes with the meta word (in LDS when they fit, else global); 31 stats twin.
-    //   61: the exact near-first stack walk (tree and stacks in LDS); 69 stats twin.
-    // Every shape's dynamic LDS ends with the lanes' running-mean slots (RT_LDS_ACC_BYTES;
-    // used by the one-pixel-per-lane kernels).
-    const size_t lds_t = (size_t)a.n_nodes * sizeof(rt_dnode);   // threaded nodes
-    const bool fits_t = lds_t <= RT_LDS_NODE_BYTES;
-    // after the nodes, as placed by the host: the Perlin table, then the media records
-    const size_t extra_end =
-        a.box_lds >= 0 ? ((size_t)a.box_lds + 5 * (size_t)a.n_box_lds) * 16
-        : a.sph_lds >= 0 ? ((size_t)a.sph_lds + 2 * (size_t)a.n_sph_lds) * 16
-        : a.media_lds >= 0 ? ((size_t)a.media_lds + 3 * (size_t)a.n_media) * 16
-        : a.perlin_lds >= 0 ? ((size_t)a.perlin_lds + ((size_t)a.tex[a.perlin_slot].w * a.tex[a.perlin_slot].h + 3) / 4) * 16
-                            : 0;
-    const size_t lds_l = (size_t)a.n_lnode_f4 * 16 > extra_end ? (size_t)a.n_lnode_f4 * 16 : extra_end;
-    const size_t lds_p = lds_t > extra_end ? lds_t : extra_end;
-    const bool stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39;
-    const bool pool = a.variant == 0 || a.variant == 39;   // the default and its stats twin
-    if (pool && !a.samples && !a.wbuf) return -1;   // pooled ordered / one-chunk units need the per-wave slots
-    const size_t acc = RT_LDS_ACC_BYTES;
-    // the launch shape and its staged bytes (before the running-mean slots)
-    enum { FAST_LDS, FAST_GLOBAL, LINK_LDS, META_LDS, META_GLOBAL } shape;
-    size_t staged;
-    const size_t stack_b = (size_t)RT_FAST_STACK * 512 * sizeof(short);
-    const size_t tree_b = (size_t)a.n_f2inner * 64 + (size_t)((a.n_f2leaves + 1) / 2) * 16;
+    // The release library has one kernel structure (tests/test_gpu_*.py pin it to the oracle):
+    // pooled samples streamed over units with walks and shading in batches (render_stream) over
+    // link-format nodes staged in LDS with the Perlin table, media, sphere and box records the
+    // host placed after them (a.lds_end_f4), 4 waves per SIMD, as 2 x 512 or 1 x 1024 threads
+    // per CU (a.block); when the nodes do not fit (a.lds_node_f4 < 2 n_nodes) the two-level
+    // walk reads the nodes below the staged top levels from global memory (1024 threads).
+    // Each in a shared-reciprocal division form (a.fastdiv) and the plain one.
+    // The A/B build (RT_AB_KNOBS) adds the other structures, all bit-identical
+    // (RT_OPTION_KERNEL_VARIANT): 37 the link walk with one pixel per lane (the round-1
+    // default), 30 threaded meta-word nodes (LDS when they fit, else global), 61 the exact
+    // near-first stack walk, and the region-timer stats twins 39 / 38 / 31 / 69.
+    enum { FAST_LDS, FAST_GLOBAL, LINK_LDS, META_LDS, META_GLOBAL, LINK_TL } shape = LINK_LDS;
+    size_t staged = (size_t)a.lds_end_f4 * 16;
+    bool stats = false, pool = true;
+    const bool tl = a.n_lnode_f4 > 0 && a.lds_node_f4 < 2 * a.n_nodes;
+    if (tl) shape = LINK_TL;
+#ifdef RT_AB_KNOBS
+    stats = a.variant == 38 || a.variant == 31 || a.variant == 69 || a.variant == 39;
+    pool = a.variant == 0 || a.variant == 39;
     if (a.variant == 61 || a.variant == 69) {
+        const size_t stack_b = (size_t)RT_FAST_STACK * 512 * sizeof(short);
+        const size_t tree_b = (size_t)a.n_f2inner * 64 + (size_t)((a.n_f2leaves + 1) / 2) * 16;
         shape = tree_b + stack_b <= RT_LDS_DYN_BYTES ? FAST_LDS : FAST_GLOBAL;
         staged = shape == FAST_LDS ? tree_b + stack_b : stack_b;
-    } else if (a.variant != 30 && a.variant != 31 && a.n_lnode_f4 > 0 &&
-               lds_l <= (a.block == 1024 ? RT_LDS_BIG_BYTES : RT_LDS_DYN_BYTES)) {
-        shape = LINK_LDS;
-        staged = lds_l;
-    } else if (fits_t && lds_p <= RT_LDS_DYN_BYTES) {
-        shape = META_LDS;
-        staged = lds_p;
-    } else {
-        shape = META_GLOBAL;
-        staged = 0;
+    } else if (a.variant == 30 || a.variant == 31 || (!pool && tl)) {
+        // threaded meta-word nodes, then what the host placed after the link-format nodes
+        const size_t lds_t = (size_t)a.n_nodes * sizeof(rt_dnode);
+        staged = std::max(lds_t, staged);
+        shape = (lds_t <= RT_LDS_NODE_BYTES && staged <= RT_LDS_DYN_BYTES) ? META_LDS : META_GLOBAL;
     }
-    const bool big = shape == LINK_LDS && pool && a.block == 1024;   // render_stream needs no running-mean slots
+    if (shape == FAST_LDS || shape == FAST_GLOBAL || shape == META_GLOBAL) {   // nothing else staged
+        if (shape == META_GLOBAL) staged = 0;
+        a.perlin_lds = a.media_lds = a.sph_lds = a.box_cmp_lds = -1;
+    }
+#endif
+    if ((shape == LINK_LDS || shape == LINK_TL) && staged > (a.block == 1024 ? RT_LDS_BIG_BYTES : RT_LDS_DYN_BYTES))
+        return -1;
+    if (shape == LINK_TL && (a.block != 1024 || !pool)) return -1;
+    if (pool && !a.samples && !a.wbuf) return -1;   // pooled ordered / one-chunk units need the per-wave slots
+    // the one-pixel-per-lane kernels (A/B) keep the lanes' running means in LDS after what is staged
     a.acc_lds = (int)(staged / 16);
-    const size_t lds = staged + (big ? 0 : acc);
-    static const bool log_shape = std::getenv("RT_LOG_SHAPE") != nullptr;   // diagnostics: the chosen launch shape
-    if (log_shape)
-        std::fprintf(stderr, "rt_launch_render: shape %d (0 fast-lds 1 fast-global 2 link 3 meta-lds 4 meta-global), "
-                             "lds %zu B, media_lds %d, perlin_lds %d, chunks %d\n",
-                     (int)shape, lds, a.media_lds, a.perlin_lds, a.n_chunks);
+    const size_t lds = staged + (pool ? 0 : RT_LDS_ACC_BYTES);
+    if (info) {
+        info[RT_LI_SHAPE] = (int)shape;
+        info[RT_LI_BLOCK] = (shape == LINK_LDS || shape == LINK_TL) ? a.block : 512;
+        info[RT_LI_FASTDIV] = a.fastdiv;
+        info[RT_LI_PRETEST] = a.box_margin > 0.0f;
+        info[RT_LI_LDS] = (int)lds;
+        info[RT_LI_LDS_NODES] = (shape == LINK_LDS || shape == LINK_TL) ? a.lds_node_f4 / 2 : 0;
+        info[RT_LI_COMPACT] = a.box_all_cmp + 2 * (a.box_cmp_lds >= 0);
+        info[RT_LI_STAGED] = a.samples != nullptr;
+        info[RT_LI_CHUNKS] = a.n_chunks;
+    }
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.
     // `a` is a pinned staging slot; same-stream ordering makes one device slot
@@ -2202,35 +2240,46 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream) {
     if (a.n_chunks > 1 && !a.samples &&
         hipMemsetAsync(a.tile_done, 0, sizeof(unsigned) * (size_t)n_tiles, st) != hipSuccess)
         return -1;
+    constexpr int SM = RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM;
     // the instantiations: <LINK, MINW, STATS, LDSN, BLOCK, FAST, OPT>
-#define RT_LAUNCH(LINK, LDSN, FAST, OPT)                                                                        \
-    (stats ? launch_persistent(render_persistent<LINK, 4, true, LDSN, 512, FAST, OPT>, 512, lds, a, d, st)    \
-           : launch_persistent(render_persistent<LINK, 4, false, LDSN, 512, FAST, OPT>, 512, lds, a, d, st))
-#define RT_LAUNCH_BIG(OPT)                                                                                       \
-    (stats ? launch_persistent(render_persistent<true, 4, true, true, 1024, false, OPT>, 1024, lds, a, d, st)  \
-           : launch_persistent(render_persistent<true, 4, false, true, 1024, false, OPT>, 1024, lds, a, d, st))
-    int rc;
+#ifdef RT_AB_KNOBS
+#define RT_KERNEL(LINK, LDSN, BLOCK, FAST, OPT)                                                                    \
+    (stats ? launch_persistent(render_persistent<LINK, 4, true, LDSN, BLOCK, FAST, OPT>, BLOCK, lds, a, d, st)  \
+           : launch_persistent(render_persistent<LINK, 4, false, LDSN, BLOCK, FAST, OPT>, BLOCK, lds, a, d, st))
+#else
+#define RT_KERNEL(LINK, LDSN, BLOCK, FAST, OPT) \
+    launch_persistent(render_persistent<LINK, 4, false, LDSN, BLOCK, FAST, OPT>, BLOCK, lds, a, d, st)
+#endif
+    int rc = -1;
+    // the link shapes x (shared-reciprocal division | plain) x (compact boxes | full box records)
+#define RT_LINK4(BLOCK, OPT)                                                                              \
+    (a.fastdiv ? (a.box_all_cmp ? RT_KERNEL(true, true, BLOCK, false, (OPT) | RT_OPT_FD | RT_OPT_BOXC)        \
+                                : RT_KERNEL(true, true, BLOCK, false, (OPT) | RT_OPT_FD))                     \
+               : (a.box_all_cmp ? RT_KERNEL(true, true, BLOCK, false, (OPT) | RT_OPT_BOXC)                    \
+                                : RT_KERNEL(true, true, BLOCK, false, (OPT))))
     switch (shape) {
-        case FAST_LDS: rc = RT_LAUNCH(false, true, true, 0); break;
-        case FAST_GLOBAL: rc = RT_LAUNCH(false, false, true, 0); break;
         case LINK_LDS:
-            if (big)
-                rc = a.fastdiv ? RT_LAUNCH_BIG(RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
-                               : RT_LAUNCH_BIG(RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM);
-            else
-            rc = pool && a.fastdiv ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_FD | RT_OPT_STREAM)
-                 : pool            ? RT_LAUNCH(true, true, false, RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM)
-                                   : RT_LAUNCH(true, true, false, 0);
+            if (!pool) {
+#ifdef RT_AB_KNOBS
+                rc = RT_KERNEL(true, true, 512, false, 0);
+#endif
+            } else if (a.block == 1024) {
+                rc = RT_LINK4(1024, SM);
+            } else {
+                rc = RT_LINK4(512, SM);
+            }
             break;
-        case META_LDS:
-            rc = pool ? RT_LAUNCH(false, true, false, RT_OPT_POOL) : RT_LAUNCH(false, true, false, 0);
-            break;
-        default:
-            rc = pool ? RT_LAUNCH(false, false, false, RT_OPT_POOL) : RT_LAUNCH(false, false, false, 0);
-            break;
+        case LINK_TL: rc = RT_LINK4(1024, SM | RT_OPT_TL); break;
+#ifdef RT_AB_KNOBS
+        case FAST_LDS: rc = RT_KERNEL(false, true, 512, true, 0); break;
+        case FAST_GLOBAL: rc = RT_KERNEL(false, false, 512, true, 0); break;
+        case META_LDS: rc = RT_KERNEL(false, true, 512, false, 0); break;
+        case META_GLOBAL: rc = RT_KERNEL(false, false, 512, false, 0); break;
+#endif
+        default: break;
     }
-#undef RT_LAUNCH
-#undef RT_LAUNCH_BIG
+#undef RT_KERNEL
+#undef RT_LINK4
     if (rc) return rc;
     if (a.samples) {   // staged chunks: the running mean over the launch's frames
         const unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);

@@ -424,6 +424,8 @@ struct rts_scene {
     World world;
     std::vector<uint8_t> buf[6];
     rts_info info{};
+    std::vector<Material> materials;   // custom scenes (rts_new): the builder's Material objects
+    bool finished = false;
 };
 
 namespace rtb {
@@ -701,6 +703,18 @@ static int max_stack_needed(const std::vector<uint8_t>& nodes) {
     return mx;
 }
 
+static void fill_info(rts_scene* s, int width, int height) {
+    World& W = s->world;
+    rts_info& I = s->info;
+    I.scene_id = s->scene_id; I.width = width; I.height = height;
+    I.n_spheres = (int)W.spheres.size(); I.n_quads = (int)W.quads.size(); I.n_boxes = (int)W.boxes.size();
+    I.n_media = (int)W.media.size(); I.n_lights = (int)W.lights.size(); I.n_bvh_nodes = (int)W.bvh_nodes.size();
+    I.n_bvh_prims = (int)W.all_models.size();
+    I.max_stack = max_stack_needed(s->buf[RT_BIND_BVH]);
+    I.n_textures = (int)W.textures.size();
+    I.background[0] = W.background.x; I.background[1] = W.background.y; I.background[2] = W.background.z;
+}
+
 }  // namespace rtb
 
 extern "C" {
@@ -743,19 +757,230 @@ int rts_build(int scene_id, int width, int height, uint64_t seed, const char* as
         return fail(RT_ERR_LIMIT, "more than 65535 records of one type");
     W.set_image_size(width, height);
     W.camera_calculate();
-    rts_info& I = s->info;
-    I.scene_id = scene_id; I.width = width; I.height = height;
-    I.n_spheres = (int)W.spheres.size(); I.n_quads = (int)W.quads.size(); I.n_boxes = (int)W.boxes.size();
-    I.n_media = (int)W.media.size(); I.n_lights = (int)W.lights.size(); I.n_bvh_nodes = (int)W.bvh_nodes.size();
-    I.n_bvh_prims = (int)W.all_models.size();
-    I.max_stack = max_stack_needed(s->buf[RT_BIND_BVH]);
-    I.n_textures = (int)W.textures.size();
-    I.background[0] = W.background.x; I.background[1] = W.background.y; I.background[2] = W.background.z;
+    fill_info(s.get(), width, height);
+    s->finished = true;
     *out = s.release();
     return RT_OK;
 }
 
 void rts_free(rts_scene* s) { delete s; }
+
+// ---- custom scenes: the reference's builder calls (Scene.java's statements) one by one
+int rts_new(uint64_t seed, const char* asset_dir, rts_scene** out) {
+    if (!out) return fail(RT_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    rts_scene* s = new rts_scene();
+    s->scene_id = -1;
+    s->world.seed = seed;
+    s->world.asset_dir = asset_dir ? asset_dir : RT_ASSET_DIR;
+    *out = s;
+    return RT_OK;
+}
+
+}  // extern "C"
+
+namespace {
+template <typename F>
+int guarded(rts_scene* s, F&& f) {
+    if (!s) return fail(RT_ERR_INVALID_ARG, "NULL scene");
+    if (s->finished) return fail(RT_ERR_STATE, "the scene was already finished (rts_finish)");
+    try {
+        return f();
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_INVALID_ARG, e.what());
+    }
+}
+Vec3f v3f(const float* p) { return Vec3f(p[0], p[1], p[2]); }
+int model_of(rts_scene* s, int handle, Model** m) {
+    if (handle < 0 || handle >= (int)s->world.pool.size()) return fail(RT_ERR_INVALID_ARG, "no such model handle");
+    *m = s->world.pool[handle].get();
+    if ((*m)->type == RT_MODEL_BVH_NODE) return fail(RT_ERR_INVALID_ARG, "no such model handle");
+    return RT_OK;
+}
+int new_model(rts_scene* s, Model* m, int* handle) {
+    // the pool's index of m (just created: a box's side quads follow it)
+    int k = (int)s->world.pool.size() - 1;
+    while (k >= 0 && s->world.pool[k].get() != m) k--;
+    if (handle) *handle = k;
+    return RT_OK;
+}
+int material_of(rts_scene* s, int handle, Material* m) {
+    if (handle < 0 || handle >= (int)s->materials.size()) return fail(RT_ERR_INVALID_ARG, "no such material handle");
+    *m = s->materials[handle];
+    return RT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rts_solid_texture(rts_scene* s, float r, float g, float b, int* tex) {
+    return guarded(s, [&] {
+        World& W = s->world;
+        if (W.solid_slot < 0) W.solid_init();
+        const int id = W.solid_register(r, g, b);
+        if (tex) *tex = id;
+        return (int)RT_OK;
+    });
+}
+
+int rts_checker_texture(rts_scene* s, const float c1[3], const float c2[3], float scale, int* tex) {
+    return guarded(s, [&] {
+        if (!c1 || !c2) return fail(RT_ERR_INVALID_ARG, "NULL colour");
+        World& W = s->world;
+        if (W.checker_slot < 0) W.checker_init();
+        const int id = W.checker_register(c1[0], c1[1], c1[2], c2[0], c2[1], c2[2], scale);
+        if (tex) *tex = id;
+        return (int)RT_OK;
+    });
+}
+
+int rts_perlin_texture(rts_scene* s, float scale, int* tex) {
+    return guarded(s, [&] {
+        const int id = s->world.perlin_create(scale);
+        if (tex) *tex = id;
+        return (int)RT_OK;
+    });
+}
+
+int rts_image_texture(rts_scene* s, const char* asset_name, int shift_x, int shift_y, int* tex) {
+    return guarded(s, [&] {
+        if (!asset_name) return fail(RT_ERR_INVALID_ARG, "NULL asset name");
+        const int id = s->world.image_create(asset_name, shift_x, shift_y);
+        if (tex) *tex = id;
+        return (int)RT_OK;
+    });
+}
+
+int rts_material(rts_scene* s, int kind, int texture, float param, const float emit[3], int* handle) {
+    return guarded(s, [&] {
+        World& W = s->world;
+        Material m;
+        switch (kind) {
+            case RT_MAT_LAMBERTIAN: m = W.lambertian(texture); break;
+            case RT_MAT_METAL: m = W.metal(texture, param); break;   // Metal.java:13: fuzz in [0, 1)
+            case RT_MAT_DIELECTRIC:
+                if (!(param >= 1.0f && param <= 2.5f))   // Dielectric.java:20-29 packs (ior - 1) / 1.5 in 16 bits
+                    return fail(RT_ERR_INVALID_ARG, "dielectric IOR must be in [1, 2.5]");
+                if (W.solid_slot < 0) W.solid_init();
+                m = W.dielectric(param);
+                break;
+            case RT_MAT_DIFFUSE_LIGHT:
+                if (!emit) return fail(RT_ERR_INVALID_ARG, "diffuse light needs an emission colour");
+                m = W.diffuse_light(emit[0], emit[1], emit[2]);
+                break;
+            case RT_MAT_ISOTROPIC: m = W.isotropic(texture); break;
+            default: return fail(RT_ERR_INVALID_ARG, "unknown material kind");
+        }
+        s->materials.push_back(m);
+        if (handle) *handle = (int)s->materials.size() - 1;
+        return (int)RT_OK;
+    });
+}
+
+int rts_sphere(rts_scene* s, const float center1[3], const float center2[3], float radius, int material, int* handle) {
+    return guarded(s, [&] {
+        Material m;
+        if (!center1) return fail(RT_ERR_INVALID_ARG, "NULL centre");
+        if (int r = material_of(s, material, &m)) return r;
+        Model* sp = s->world.sphere(v3f(center1), center2 ? v3f(center2) : v3f(center1), radius, m);
+        return new_model(s, sp, handle);
+    });
+}
+
+int rts_quad(rts_scene* s, const float q[3], const float u[3], const float v[3], int material, int* handle) {
+    return guarded(s, [&] {
+        Material m;
+        if (!q || !u || !v) return fail(RT_ERR_INVALID_ARG, "NULL vector");
+        if (int r = material_of(s, material, &m)) return r;
+        return new_model(s, s->world.quad(v3f(q), v3f(u), v3f(v), m), handle);
+    });
+}
+
+int rts_box(rts_scene* s, const float a[3], const float b[3], const float translation[3], const float rotation[3],
+            int material, int* handle) {
+    return guarded(s, [&] {
+        Material m;
+        if (!a || !b) return fail(RT_ERR_INVALID_ARG, "NULL corner");
+        if ((translation == nullptr) != (rotation == nullptr))
+            return fail(RT_ERR_INVALID_ARG, "Box.java takes translation and rotation together");
+        if (int r = material_of(s, material, &m)) return r;
+        Vec3f t, rot;
+        if (translation) { t = v3f(translation); rot = v3f(rotation); }
+        Model* bx = s->world.box(v3f(a), v3f(b), translation ? &t : nullptr, rotation ? &rot : nullptr, m);
+        return new_model(s, bx, handle);
+    });
+}
+
+int rts_constant_medium(rts_scene* s, int boundary, float density, int material, int* handle) {
+    return guarded(s, [&] {
+        Material m;
+        Model* bnd = nullptr;
+        if (int r = model_of(s, boundary, &bnd)) return r;
+        if (bnd->type == RT_MODEL_CONSTANT_MEDIUM) return fail(RT_ERR_INVALID_ARG, "a medium cannot bound a medium");
+        if (int r = material_of(s, material, &m)) return r;
+        if (!(density > 0.0f)) return fail(RT_ERR_INVALID_ARG, "density must be positive");
+        // ConstantMedium.java:12-20: the constructor registers its boundary with addModel
+        return new_model(s, s->world.constant_medium(bnd, density, m), handle);
+    });
+}
+
+int rts_add_model(rts_scene* s, int handle) {
+    return guarded(s, [&] {
+        Model* m = nullptr;
+        if (int r = model_of(s, handle, &m)) return r;
+        s->world.add_model(m);
+        return (int)RT_OK;
+    });
+}
+
+int rts_add_light(rts_scene* s, int handle) {
+    return guarded(s, [&] {
+        Model* m = nullptr;
+        if (int r = model_of(s, handle, &m)) return r;
+        if (m->type != RT_MODEL_SPHERE && m->type != RT_MODEL_QUAD)
+            return fail(RT_ERR_INVALID_ARG, "lights are spheres or quads (pdf.glsl:58-96)");
+        s->world.add_light(m);
+        return (int)RT_OK;
+    });
+}
+
+int rts_camera(rts_scene* s, const rts_camera_params* p) {
+    return guarded(s, [&] {
+        if (!p) return fail(RT_ERR_INVALID_ARG, "NULL camera");
+        World& W = s->world;
+        W.look_from = v3f(p->look_from);
+        W.look_at = v3f(p->look_at);
+        W.vup = v3f(p->vup);
+        W.vfov = p->vfov;
+        W.defocus_angle = p->defocus_angle;
+        W.focus_dist = p->focus_dist;
+        W.background = v3f(p->background);
+        return (int)RT_OK;
+    });
+}
+
+int rts_finish(rts_scene* s, int width, int height) {
+    if (!s) return fail(RT_ERR_INVALID_ARG, "NULL scene");
+    if (s->scene_id >= 0 || s->finished) return fail(RT_ERR_STATE, "only an unfinished rts_new scene can be finished");
+    if (width <= 0 || height <= 0) return fail(RT_ERR_INVALID_ARG, "image size must be positive");
+    World& W = s->world;
+    try {
+        put_models_to_program(s);
+        W.solid_put_data();
+        W.checker_put_data();
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_INVALID_ARG, e.what());
+    }
+    if (W.textures.size() > RT_MAX_TEXTURES) return fail(RT_ERR_LIMIT, "more than 8 textures");
+    if (W.spheres.size() > RT_MAX_RECORDS || W.quads.size() > RT_MAX_RECORDS || W.boxes.size() > RT_MAX_RECORDS ||
+        W.media.size() > RT_MAX_RECORDS || W.bvh_nodes.size() > RT_MAX_RECORDS)
+        return fail(RT_ERR_LIMIT, "more than 65535 records of one type");
+    W.set_image_size(width, height);
+    W.camera_calculate();
+    fill_info(s, width, height);
+    s->finished = true;
+    return RT_OK;
+}
 
 int rts_get_info(const rts_scene* s, rts_info* info) {
     if (!s || !info) return fail(RT_ERR_INVALID_ARG, "NULL argument");

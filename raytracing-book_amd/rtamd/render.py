@@ -62,11 +62,27 @@ def deinterleave(gathered, height, world, stripe_rows):
     return out
 
 
-class RenderContext:
-    """An rt_ctx: device buffers, accumulation image and launch state."""
+# rt_debug.h RT_OPTION_*: per-context options set by explicit calls (the release library
+# reads no environment).  Below 100 they never change a bit of the image; 100+ exist in
+# the A/B build only.
+OPTIONS = {"box_pretest": 1, "fastdiv": 2, "sph_lds": 3, "big_wg": 4, "chunk_target": 5,
+           "staged_chunk_target": 6, "stage_tiles": 7, "sm_batch": 8, "sm_frac": 9, "walk_frac": 10,
+           "watchdog_ms": 11, "chunk_wait_ms": 12, "lds_node_cap": 13, "compact_boxes": 14,
+           "kernel_variant": 100, "debug_flags": 101}
+# rt_debug_last_launch fields
+LAUNCH_FIELDS = ("shape", "block", "fastdiv", "pretest", "lds_bytes", "lds_nodes", "box_records", "staged",
+                 "chunks")
+SHAPES = {0: "fast-lds", 1: "fast-global", 2: "link-lds", 3: "meta-lds", 4: "meta-global", 5: "link-two-level"}
 
-    def __init__(self, devices=(0,), rank=0, world=1, stripe_rows=16):
-        L = _lib.amd()
+
+class RenderContext:
+    """An rt_ctx: device buffers, accumulation image and launch state.
+
+    ``options`` (dict name -> int, see OPTIONS) are applied right after creation;
+    ``ab=True`` uses the A/B build (librtamd_ab.so) for kernel-variant options."""
+
+    def __init__(self, devices=(0,), rank=0, world=1, stripe_rows=16, options=None, ab=False):
+        L = _lib.amd_ab() if ab else _lib.amd()
         self._L = L
         devs = (ctypes.c_int * len(devices))(*devices)
         h = ctypes.c_void_p()
@@ -82,6 +98,25 @@ class RenderContext:
         self.max_depth = 5
         self.background = np.zeros(3, np.float32)
         self.sqrt_spp, self.recip_sqrt_spp = 1.0, 1.0
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
+
+    def set_option(self, name, value):
+        """rt_debug_set_option (rt_debug.h RT_OPTION_*)."""
+        self._check(self._L.rt_debug_set_option(self._h, OPTIONS[name], int(value)))
+
+    def get_option(self, name):
+        v = ctypes.c_int()
+        self._check(self._L.rt_debug_get_option(self._h, OPTIONS[name], ctypes.byref(v)))
+        return v.value
+
+    def last_launch(self):
+        """rt_debug_last_launch as a dict (the launch shape the last rt_render took)."""
+        out = (ctypes.c_int * 16)()
+        self._check(self._L.rt_debug_last_launch(self._h, out, 16))
+        d = dict(zip(LAUNCH_FIELDS, out[:len(LAUNCH_FIELDS)]))
+        d["shape_name"] = SHAPES.get(d["shape"], "?")
+        return d
 
     def _check(self, rc):
         if rc != 0:
@@ -105,13 +140,16 @@ class RenderContext:
         assert ubo.size == 28
         self._check(self._L.rt_set_camera(self._h, ubo.ctypes.data_as(c_float_p)))
 
-    def set_params(self, max_depth=None, background=None, spp=None):
+    def set_params(self, max_depth=None, background=None, spp=None, uniforms=None):
+        """uniforms = (sqrt_spp, recip_sqrt_spp) as raw floats, instead of spp's."""
         if max_depth is not None:
             self.max_depth = int(max_depth)
         if background is not None:
             self.background = np.asarray(background, np.float32)
         if spp is not None:
             self.sqrt_spp, self.recip_sqrt_spp = spp_uniforms(spp)
+        if uniforms is not None:
+            self.sqrt_spp, self.recip_sqrt_spp = float(np.float32(uniforms[0])), float(np.float32(uniforms[1]))
         bg = np.ascontiguousarray(self.background, dtype=np.float32)
         self._check(self._L.rt_set_params(self._h, self.max_depth, bg.ctypes.data_as(c_float_p),
                                           self.sqrt_spp, self.recip_sqrt_spp))

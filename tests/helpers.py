@@ -12,9 +12,10 @@ def oracle_image(scene, frames, max_depth=5, spp=None, first_frame=1, seed=1, **
     return pyoracle.render(o, rf, first_frame=first_frame, **kw)
 
 
-def gpu_image(scene, frames, max_depth=5, spp=None, first_frame=1, seed=1, devices=(0,), chunks=None):
+def gpu_image(scene, frames, max_depth=5, spp=None, first_frame=1, seed=1, devices=(0,), chunks=None, options=None,
+              ab=False):
     spp = spp or frames
-    ctx = rtamd.RenderContext(devices=devices)
+    ctx = rtamd.RenderContext(devices=devices, options=options, ab=ab)
     ctx.upload_scene(scene)
     ctx.set_params(max_depth=max_depth, spp=spp)
     ctx.resize(scene.width, scene.height)

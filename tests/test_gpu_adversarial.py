@@ -1,0 +1,132 @@
+"""Adversarial parity: the kernel's exactness shortcuts against rays aimed at what
+could break them (tests/adversarial.py), through the C ABI, bit for bit against
+the CPU oracle.
+
+The shortcuts and what each case aims at:
+  * the box bounds pre-test (its margin argument): box edges and corners hit
+    exactly, grazing faces, t at tmin, extents near 2^20;
+  * the shared-reciprocal division (rcp_nr / div_nr): the same, with the regime
+    check proven by a scene just inside 2^20 (on) and one just past (off);
+  * the compact box records (box_test_compact): canonical boxes at exact edges,
+    grazing and t = tmin; rotated boxes take the full records;
+  * the link-format walk beyond 2047 nodes, in LDS (~4000 nodes) and two-level
+    (~9800 nodes: top levels in LDS, the rest from global memory).
+Every case renders with the default options and with each shortcut turned off
+(rt_debug.h RT_OPTION_*); all must equal the oracle.  The launch each default
+render took is asserted (rt_debug_last_launch), so a case cannot pass by
+silently taking another path.
+"""
+import numpy as np
+import pytest
+
+import adversarial
+import pyoracle
+import rtamd
+from helpers import bit_equal, mismatch_report
+
+pytestmark = pytest.mark.gpu
+
+CASES = adversarial.cases()
+OFF = [{}, {"box_pretest": 0}, {"fastdiv": 0}, {"compact_boxes": 0}]
+
+
+def oracle(case):
+    o = pyoracle.OracleScene(case.scene, max_depth=case.depth, uniforms=case.uniforms)
+    return pyoracle.render(o, rtamd.frame_rand_factors(1, 0, case.frames))
+
+
+def render(case, options=None):
+    ctx = rtamd.RenderContext(devices=(0,), options=options)
+    ctx.upload_scene(case.scene)
+    ctx.set_params(max_depth=case.depth, uniforms=case.uniforms)
+    ctx.resize(case.scene.width, case.scene.height)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, case.frames))
+    img = ctx.read_image()
+    info = ctx.last_launch()
+    ctx.close()
+    return img, info
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c.name for c in CASES])
+def test_adversarial_case_matches_oracle(gpu, case):
+    ref = oracle(case)
+    for opts in OFF:
+        out, info = render(case, opts)
+        assert bit_equal(out, ref), f"{case.name} {opts or 'default'}: {mismatch_report(out, ref)}"
+        if not opts:
+            for k, v in case.expect.items():
+                assert info[k] == v, f"{case.name}: launch {k} = {info[k]}, expected {v} ({info})"
+
+
+@pytest.mark.parametrize("cap", [4096, 32768, 65536])
+def test_two_level_walk_forced(gpu, cap):
+    """The ~4000-node cloud, which fits LDS, with only `cap` bytes of its nodes staged:
+    the same bits as the oracle whatever the split between LDS and global nodes."""
+    case = next(c for c in CASES if c.name == "bvh_4k_lds")
+    ref = oracle(case)
+    out, info = render(case, {"lds_node_cap": cap})
+    assert info["shape_name"] == "link-two-level" and info["lds_nodes"] == cap // 32, info
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
+def test_watchdog_fault_is_reported(gpu):
+    """A progress bound of 0 trips every wave's first check: rt_sync reports the fault
+    (RT_ERR_DEVICE), and the context renders correctly again with the bound restored."""
+    s = rtamd.Scene(8, 64, 48, seed=1)
+    ref = pyoracle.render(pyoracle.OracleScene(s, max_depth=5, spp=4), rtamd.frame_rand_factors(1, 0, 4))
+    ctx = rtamd.RenderContext(options={"watchdog_ms": 0})
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=4)
+    ctx.resize(64, 48)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+    with pytest.raises(rtamd.RTError, match="watchdog") as e:
+        ctx.sync()
+    assert e.value.code == -2
+    ctx.set_option("watchdog_ms", 120000)
+    ctx.resize(64, 48)                     # a fresh zero image
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+    out = ctx.read_image()
+    ctx.close()
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
+def test_chunk_wait_fault_is_reported(gpu):
+    """Ordered one-frame chunks of one tile with a wait bound of 0: a wave that finds its
+    tile's previous chunk unpublished stops waiting and sets the fault word."""
+    s = rtamd.Scene(8, 8, 8, seed=1)
+    ctx = rtamd.RenderContext(options={"chunk_wait_ms": 0, "stage_tiles": 0, "chunk_target": 100000})
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=256)
+    ctx.resize(8, 8)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 256))
+    with pytest.raises(rtamd.RTError, match="ordered-chunk wait") as e:
+        ctx.sync()
+    assert e.value.code == -2
+    ctx.close()
+
+
+def test_rand_factors_and_sizes_are_validated(gpu):
+    """Inputs that would freeze rand() on the device (random.glsl:2-7) are rejected."""
+    s = rtamd.Scene(6, 8, 8, seed=1)
+    ctx = rtamd.RenderContext()
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=4)
+    ctx.resize(8, 8)
+    for bad in (np.nan, np.inf, -np.inf, 2048.0):
+        rf = rtamd.frame_rand_factors(1, 0, 3)
+        rf[1] = bad
+        with pytest.raises(rtamd.RTError, match="rand_factors"):
+            ctx.render(1, rf)
+    with pytest.raises(rtamd.RTError, match="bad image size"):
+        ctx.resize(65537, 1)
+    ctx.close()
+
+
+def test_release_library_has_no_ab_options(gpu):
+    """The release library: no kernel variants, no ablations, no stats kernels."""
+    assert rtamd.amd().rt_debug_ab_build() == 0 and rtamd.amd_ab().rt_debug_ab_build() == 1
+    ctx = rtamd.RenderContext()
+    for name in ("kernel_variant", "debug_flags"):
+        with pytest.raises(rtamd.RTError, match="unknown option"):
+            ctx.set_option(name, 0)
+    ctx.close()

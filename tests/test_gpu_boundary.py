@@ -141,54 +141,57 @@ def test_bound_torch_image_and_stream(gpu):
 VARIANTS = [0, 37, 30, 61]   # streamed batched pooled samples (default), one pixel per lane (round-1 default), threaded meta walk, exact near-first walk
 
 
-# work splits (rt_capi.hip rt_render): one unit per tile with all frames (folded per
-# wave), ordered frame chunks handed over between waves, staged chunks (the default)
+# work splits (rt_capi.hip rt_render; rt_debug.h RT_OPTION_*): one unit per tile with all
+# frames (folded per wave), ordered frame chunks handed over between waves, staged chunks
+# (the default)
 SPLITS = {
-    "direct": {"RT_CHUNK_TARGET": "0"},
-    "ordered1": {"RT_STAGE_TILES": "0", "RT_CHUNK_TARGET": "1"},
-    "ordered16": {"RT_STAGE_TILES": "0", "RT_CHUNK_TARGET": "16"},
-    "ordered_max": {"RT_STAGE_TILES": "0", "RT_CHUNK_TARGET": "100000"},
+    "direct": {"chunk_target": 0},
+    "ordered1": {"stage_tiles": 0, "chunk_target": 1},
+    "ordered16": {"stage_tiles": 0, "chunk_target": 16},
+    "ordered_max": {"stage_tiles": 0, "chunk_target": 100000},
     "staged": {},
-    "staged_max": {"RT_STAGED_CHUNK_TARGET": "100000"},
+    "staged_max": {"staged_chunk_target": 100000},
 }
 
 
 @pytest.mark.parametrize("sid", [8, 6, 7])
 @pytest.mark.parametrize("split", list(SPLITS))
-def test_all_kernel_variants_identical(gpu, monkeypatch, split, sid):
-    """Every launch shape of the kernel (RT_KERNEL_VARIANT) and every work split
-    (SPLITS) renders the same bits; scenes 8 (canonical boxes, media, Perlin, image
-    texture), 6 and 7 (rotated boxes: the general box test)."""
+def test_all_kernel_variants_identical(gpu, split, sid):
+    """The release kernel under every work split (SPLITS), and every structure of the A/B
+    build (RT_OPTION_KERNEL_VARIANT, librtamd_ab.so) render the same bits; scenes 8
+    (canonical boxes, media, Perlin, image texture), 6 and 7 (rotated boxes: the general
+    box test)."""
     s = rtamd.Scene(sid, 40, 24, seed=1)
     ref = oracle_image(s, 6)
-    for k, v in SPLITS[split].items():
-        monkeypatch.setenv(k, v)
+    out = gpu_image(s, 6, options=SPLITS[split])
+    assert bit_equal(out, ref), f"release, split {split}: {mismatch_report(out, ref)}"
     for v in VARIANTS:
-        monkeypatch.setenv("RT_KERNEL_VARIANT", str(v))
-        out = gpu_image(s, 6)
-        assert bit_equal(out, ref), f"variant {v}, split {split}: {mismatch_report(out, ref)}"
+        out = gpu_image(s, 6, options=dict(SPLITS[split], kernel_variant=v), ab=True)
+        assert bit_equal(out, ref), f"A/B variant {v}, split {split}: {mismatch_report(out, ref)}"
 
 
 @pytest.mark.parametrize("split", ["ordered_max", "staged_max"])
-def test_chunk_chain_small_image(gpu, monkeypatch, split):
+def test_chunk_chain_small_image(gpu, split):
     """Few tiles, many chunks: each of the 15 tiles' 600 frames in one-frame chunks over
     2 launches (300 + 300 frames): ordered, every chunk waits for the previous one (the
     hand-off is on the critical path; render_stream folds two units per wave in claim
     order); staged, every chunk's colours folded by fold_kernel."""
     s = rtamd.Scene(8, 40, 24, seed=1)
     ref = oracle_image(s, 600, spp=600)
-    for k, v in SPLITS[split].items():
-        monkeypatch.setenv(k, v)
-    out = gpu_image(s, 600, spp=600)
+    out = gpu_image(s, 600, spp=600, options=SPLITS[split])
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
 def test_stats_build_renders_same_bits(gpu):
-    """The diagnostic build (rt_debug_enable_stats) changes timing only."""
+    """The diagnostic build (rt_debug_enable_stats, A/B library) changes timing only; the
+    release library has no stats kernels."""
     s = rtamd.Scene(8, 40, 24, seed=1)
     ref = oracle_image(s, 2)
-    L = rtamd.amd()
-    ctx = rtamd.RenderContext()
+    rel = rtamd.RenderContext()
+    assert rtamd.amd().rt_debug_enable_stats(rel._h, 1) == -3
+    rel.close()
+    L = rtamd.amd_ab()
+    ctx = rtamd.RenderContext(ab=True)
     assert L.rt_debug_enable_stats(ctx._h, 1) == 0
     ctx.upload_scene(s)
     ctx.set_params(max_depth=5, spp=2)

@@ -24,10 +24,8 @@ pytestmark = pytest.mark.gpu
 STRIPE = 8
 
 
-def render(scene, frames, depth, spp, rank=0, world=1, stripe=16, chunk_target=None, monkeypatch=None):
-    if chunk_target is not None:
-        monkeypatch.setenv("RT_CHUNK_TARGET", str(chunk_target))
-    ctx = rtamd.RenderContext(devices=(0,), rank=rank, world=world, stripe_rows=stripe)
+def render(scene, frames, depth, spp, rank=0, world=1, stripe=16, options=None):
+    ctx = rtamd.RenderContext(devices=(0,), rank=rank, world=world, stripe_rows=stripe, options=options)
     ctx.upload_scene(scene)
     ctx.set_params(max_depth=depth, spp=spp)
     ctx.resize(scene.width, scene.height)
@@ -64,13 +62,13 @@ CONFIGS = [
 
 
 @pytest.mark.parametrize("name,sid,w,h,frames,spp,depth", CONFIGS, ids=[c[0] for c in CONFIGS])
-def test_full_size_sampled_rows_match_oracle(gpu, monkeypatch, name, sid, w, h, frames, spp, depth):
+def test_full_size_sampled_rows_match_oracle(gpu, name, sid, w, h, frames, spp, depth):
     scene = rtamd.Scene(sid, w, h, seed=1)
     n_stripes = (h + STRIPE - 1) // STRIPE
     rng = np.random.default_rng(sid * 7 + w)
     stripes = sorted({0, n_stripes - 1, *rng.choice(n_stripes, 3, replace=False).tolist()})
-    direct = render(scene, frames, depth, spp, chunk_target=0, monkeypatch=monkeypatch)
-    chunked = render(scene, frames, depth, spp, chunk_target=64, monkeypatch=monkeypatch)
+    direct = render(scene, frames, depth, spp, options={"chunk_target": 0})
+    chunked = render(scene, frames, depth, spp, options={"chunk_target": 64})
     assert bit_equal(direct, chunked), "direct vs chunked: " + mismatch_report(direct, chunked)
     ref = oracle_rows(scene, frames, depth, spp, stripes)
     check_rows(direct, ref, stripes, h)
@@ -90,43 +88,38 @@ def test_full_size_stripe_partition_equals_one_gpu(gpu, world):
 
 
 @pytest.mark.parametrize("sid", [8, 0])
-def test_ordered_chunks_equal_whole_launch_1080p(gpu, monkeypatch, sid):
+def test_ordered_chunks_equal_whole_launch_1080p(gpu, sid):
     """64 frames at 1080p as 64 one-frame chunks per tile (32 400 tiles, 63 wave-to-wave
     hand-offs each, every chunk on whichever CU/XCD dequeues it) == one unit per tile
     == 64 staged one-frame chunks per tile (the default's split, at its extreme)."""
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
-    whole = render(scene, 64, 5, 4096, chunk_target=0, monkeypatch=monkeypatch)
-    monkeypatch.setenv("RT_STAGE_TILES", "0")
-    chunked = render(scene, 64, 5, 4096, chunk_target=100000, monkeypatch=monkeypatch)
+    whole = render(scene, 64, 5, 4096, options={"chunk_target": 0})
+    chunked = render(scene, 64, 5, 4096, options={"stage_tiles": 0, "chunk_target": 100000})
     assert bit_equal(chunked, whole), mismatch_report(chunked, whole)
-    monkeypatch.delenv("RT_STAGE_TILES")
-    monkeypatch.setenv("RT_STAGED_CHUNK_TARGET", "100000")
-    staged = render(scene, 64, 5, 4096, chunk_target=16, monkeypatch=monkeypatch)
+    staged = render(scene, 64, 5, 4096, options={"staged_chunk_target": 100000, "chunk_target": 16})
     assert bit_equal(staged, whole), mismatch_report(staged, whole)
 
 
 @pytest.mark.parametrize("sid", [8, 6, 7])
-@pytest.mark.parametrize("knob", ["RT_BOX_PRETEST", "RT_FASTDIV"])
-def test_exactness_shortcuts_change_no_bit_1080p(gpu, monkeypatch, knob, sid):
-    """The box bounds pre-test and the shared-reciprocal divisions against
-    the plain tests, whole 1080p images (every ray of 8 frames): scene 8 (ground boxes
-    seen at grazing angles), 6 and 7 (rotated boxes): the same bits."""
+@pytest.mark.parametrize("knob", ["box_pretest", "fastdiv", "compact_boxes"])
+def test_exactness_shortcuts_change_no_bit_1080p(gpu, knob, sid):
+    """The box bounds pre-test, the shared-reciprocal divisions and the compact box records
+     against the plain tests, whole 1080p images (every ray of 8 frames): scene 8
+    (ground boxes seen at grazing angles), 6 and 7 (rotated boxes): the same bits."""
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
     on = render(scene, 8, 5, 4096)
-    monkeypatch.setenv(knob, "0")
-    off = render(scene, 8, 5, 4096)
+    off = render(scene, 8, 5, 4096, options={knob: 0})
     assert bit_equal(on, off), mismatch_report(on, off)
 
 
 @pytest.mark.parametrize("sid", [8, 0])
-@pytest.mark.parametrize("knob", ["RT_BIG_WG", "RT_SPH_LDS"])
-def test_lds_record_copies_change_no_bit_1080p(gpu, monkeypatch, knob, sid):
+@pytest.mark.parametrize("knob", ["big_wg", "sph_lds"])
+def test_lds_record_copies_change_no_bit_1080p(gpu, knob, sid):
     """The leaf tests' records read from LDS: scene 8 runs as one 1024-thread
     workgroup per CU with its spheres' and canonical boxes' records staged beside the nodes,
     scene 0 stages its spheres in the 512-thread shape.  Against the global-memory reads
     (knob = 0), whole 1080p images of 8 frames: the same bits."""
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
     on = render(scene, 8, 5, 4096)
-    monkeypatch.setenv(knob, "0")
-    off = render(scene, 8, 5, 4096)
+    off = render(scene, 8, 5, 4096, options={knob: 0})
     assert bit_equal(on, off), mismatch_report(on, off)

@@ -1,5 +1,5 @@
-"""The link-format node loop (RT_KERNEL_VARIANT=37, rt_kernel.hip trace with
-WHILE_WHILE bit 8; nodes from rt_capi.hip build_links).
+"""The link-format node loop of the A/B build's variant 37 (rt_kernel.hip trace;
+nodes from rt_capi.hip build_links) against the threaded meta-word walk (30).
 
 It walks the reference's threaded BVH in the same node order as variant 30,
 only with explicit hit / miss successors and packed slab arithmetic, so the
@@ -15,9 +15,8 @@ from helpers import bit_equal, mismatch_report
 pytestmark = pytest.mark.gpu
 
 
-def render(monkeypatch, variant, scene, frames, depth=5):
-    monkeypatch.setenv("RT_KERNEL_VARIANT", str(variant))
-    ctx = rtamd.RenderContext(devices=(0,))
+def render(variant, scene, frames, depth=5):
+    ctx = rtamd.RenderContext(devices=(0,), options={"kernel_variant": variant}, ab=True)
     ctx.upload_scene(scene)
     ctx.set_params(max_depth=depth, spp=frames)
     ctx.resize(scene.width, scene.height)
@@ -28,8 +27,8 @@ def render(monkeypatch, variant, scene, frames, depth=5):
 
 
 @pytest.mark.parametrize("sid,frames", [(8, 16), (0, 8), (2, 4), (6, 4), (9, 8)])
-def test_link_walk_equals_threaded_walk_1080p(gpu, monkeypatch, sid, frames):
+def test_link_walk_equals_threaded_walk_1080p(gpu, sid, frames):
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
-    ref = render(monkeypatch, 30, scene, frames)
-    out = render(monkeypatch, 37, scene, frames)
+    ref = render(30, scene, frames)
+    out = render(37, scene, frames)
     assert bit_equal(out, ref), mismatch_report(out, ref)

@@ -1,12 +1,16 @@
 """The link-format BVH the default kernel walks (rt_capi.hip build_links,
-rt_device.h RT_LINK_*; rt_kernel.hip trace with WHILE_WHILE bit 8) — host-side,
-no GPU needed.
+rt_device.h RT_LINK_*; rt_kernel.hip link_walk) — host-side, no GPU needed.
 
-Every node keeps the threaded node's box; its hit / miss words are the
-threaded walk's successors as byte offsets, and a hit leaf leaves the loop
-with its leaf ordinal.  Under any pattern of box hits the link walk visits the
-same nodes and tests the same leaves, in the same order, as the threaded walk
-(which itself replays the reference's stack walk, test_abi.py).
+Every node keeps its threaded node's box and is placed breadth-first (the
+root's level first, an inner node's right child before its left one), so a
+two-level launch stages the top levels every ray walks as one LDS prefix.
+Its hit / miss words are the threaded walk's successors as byte addresses; a
+hit leaf leaves the loop with its leaf ordinal, and the leaf's record holds its
+prim types and the address the walk continues at.  Under any pattern of box
+hits the link walk visits the same nodes and tests the same leaves, in the same
+order, as the threaded walk (which itself replays the reference's stack walk,
+test_abi.py) — for the shipped scenes and for BVHs up to the reference's 16-bit
+limit of 65535 nodes (the round-2 format stopped at 2047).
 """
 import ctypes
 
@@ -16,18 +20,39 @@ import pytest
 import rtamd
 from test_fast_tables import END, is_leaf, threaded
 
-LEAF, LEND = 0x80000000, 0xFFFFFFFF
+LEAF, LEND, NEXT_END = 0x80000000, 0xFFFFFFFF, 0xFFFFFF
 
 
-def links(scene):
+def links_of(bvh_bytes):
     L = rtamd.amd()
-    b = scene.buffers[1]
-    bvh = ctypes.create_string_buffer(b, len(b))
+    bvh = ctypes.create_string_buffer(bvh_bytes, len(bvh_bytes))
     n = ctypes.c_int()
-    assert L.rt_debug_link_nodes(bvh, len(b), None, 0, ctypes.byref(n)) == 0
+    assert L.rt_debug_link_nodes(bvh, len(bvh_bytes), None, 0, ctypes.byref(n)) == 0
     out = np.zeros((max(n.value, 1), 4), np.float32)
-    assert L.rt_debug_link_nodes(bvh, len(b), out.ctypes.data, out.nbytes, ctypes.byref(n)) == 0
+    assert L.rt_debug_link_nodes(bvh, len(bvh_bytes), out.ctypes.data, out.nbytes, ctypes.byref(n)) == 0
     return out[:n.value]
+
+
+def threaded_of(bvh_bytes):
+    L = rtamd.amd()
+    n = ctypes.c_int()
+    assert L.rt_debug_threaded_bvh(bvh_bytes, len(bvh_bytes), None, 0, ctypes.byref(n)) == 0
+    from test_fast_tables import DN
+    out = np.zeros(n.value, DN)
+    assert L.rt_debug_threaded_bvh(bvh_bytes, len(bvh_bytes), out.ctypes.data, out.nbytes, ctypes.byref(n)) == 0
+    return out
+
+
+def bfs_order(tn):
+    """Breadth-first order of the threaded nodes: an inner node k's children are its
+    right child k + 1 and its left child skip(k + 1)."""
+    order, h = [0], 0
+    while h < len(order):
+        k = order[h]
+        h += 1
+        if not is_leaf(tn[k]):
+            order += [k + 1, int(tn[k + 1]["meta"]) & 0xFFFF]
+    return order
 
 
 def walk_threaded(tn, hits):
@@ -39,71 +64,83 @@ def walk_threaded(tn, hits):
         if not hits[i]:
             i = skip
         elif is_leaf(nd):
-            tested.append((int(nd["meta"]) & 0xFF0000, int(nd["prims"])))
+            tested.append((int(nd["meta"]) >> 16 & 0xFF, int(nd["prims"])))
             i = skip
         else:
             i += 1
     return seen, tested
 
 
-def walk_links(ln, n, hits):
+def walk_links(ln, n, hits, node_of_slot):
+    """The kernel's loop (render_stream): nodes by address, leaves by ordinal."""
     words = ln.view(np.uint32)
     leaves = words[2 * n:].reshape(-1, 2)
     nx, seen, tested = 0, [], []
     while True:
         while nx < LEAF:
-            k = nx // 32
+            k = node_of_slot[nx // 32]
             seen.append(k)
-            nx = int(words[2 * k + 1, 2] if hits[k] else words[2 * k + 1, 3])
+            nx = int(words[2 * (nx // 32) + 1, 2] if hits[k] else words[2 * (nx // 32) + 1, 3])
         if nx == LEND:
             break
-        lf = leaves[(nx >> 16) & 0x7FFF]
-        tested.append((int(lf[0]), int(lf[1])))
-        nx &= 0xFFFF
-        if nx == 0xFFFF:
+        lf = leaves[nx & 0x7FFFFFFF]
+        tested.append((int(lf[0]) & 0xFF, int(lf[1])))
+        nx = int(lf[0]) >> 8
+        if nx == NEXT_END:
             break
     return seen, tested
+
+
+def check_layout(tn, ln):
+    n = len(tn)
+    order = bfs_order(tn)
+    assert sorted(order) == list(range(n))
+    pos = np.empty(n, np.int64)
+    pos[order] = np.arange(n)
+    n_leaves = sum(is_leaf(nd) for nd in tn)
+    assert len(ln) == 2 * n + (n_leaves + 1) // 2
+    boxes = ln[:2 * n].reshape(n, 8)[:, :6]
+    assert np.array_equal(boxes.view(np.uint32), np.stack([tn[k]["box"] for k in order]).view(np.uint32))
+    w = ln.view(np.uint32)
+    leaves = w[2 * n:].reshape(-1, 2)
+    li = 0
+    for k, nd in enumerate(tn):
+        skip = int(nd["meta"]) & 0xFFFF
+        at = 2 * pos[k] + 1
+        assert int(w[at, 3]) == (LEND if skip == END else 32 * pos[skip])
+        if is_leaf(nd):
+            assert int(w[at, 2]) == LEAF | li
+            assert int(leaves[li, 0]) == (int(nd["meta"]) >> 16 & 0xFF) | (NEXT_END if skip == END else 32 * pos[skip]) << 8
+            assert int(leaves[li, 1]) == int(nd["prims"])
+            li += 1
+        else:
+            assert int(w[at, 2]) == 32 * pos[k + 1]
+    return order
 
 
 @pytest.mark.parametrize("sid", range(10))
 def test_link_format_matches_threaded_nodes(sid):
     scene = rtamd.Scene(sid, 64, 36, seed=1)
-    tn = threaded(scene)
-    ln = links(scene)
-    n = len(tn)
-    n_leaves = sum(is_leaf(nd) for nd in tn)
-    assert len(ln) == 2 * n + (n_leaves + 1) // 2
-    boxes = ln[:2 * n].reshape(n, 8)[:, :6]
-    assert np.array_equal(boxes.view(np.uint32), np.stack([nd["box"] for nd in tn]).view(np.uint32))
-    w = ln.view(np.uint32)
-    li = 0
-    for k, nd in enumerate(tn):
-        skip = int(nd["meta"]) & 0xFFFF
-        miss = LEND if skip == END else 32 * skip
-        assert int(w[2 * k + 1, 3]) == miss
-        if is_leaf(nd):
-            assert int(w[2 * k + 1, 2]) == LEAF | li << 16 | (0xFFFF if skip == END else 32 * skip)
-            li += 1
-        else:
-            assert int(w[2 * k + 1, 2]) == 32 * (k + 1)
+    check_layout(threaded(scene), links_of(scene.buffers[1]))
 
 
 @pytest.mark.parametrize("sid", [0, 4, 6, 8])
 def test_link_walk_replays_threaded_walk(sid):
     scene = rtamd.Scene(sid, 64, 36, seed=1)
     tn = threaded(scene)
-    ln = links(scene)
+    ln = links_of(scene.buffers[1])
+    order = check_layout(tn, ln)
     rng = np.random.default_rng(sid)
     for p in (0.0, 0.3, 0.7, 1.0):
         for _ in range(20):
             hits = rng.random(len(tn)) < p
-            assert walk_links(ln, len(tn), hits) == walk_threaded(tn, hits)
+            assert walk_links(ln, len(tn), hits, order) == walk_threaded(tn, hits)
 
 
 def heap_bvh(n_leaves):
     """A complete reference BVH (BVHNode std430 records) with n_leaves sphere leaves, heap order."""
     n_inner = n_leaves - 1
-    rec = np.zeros(n_inner + n_leaves, dtype=[("box", "<f4", 6), ("l", "<i4"), ("r", "<i4")])
+    rec = np.zeros(n_inner + n_leaves, dtype=[("box", "<f4", 6), ("l", "<u4"), ("r", "<u4")])
     rec["box"] = [-1, 1, -1, 1, -1, 1]
     for k in range(n_inner):
         rec[k]["l"], rec[k]["r"] = (2 * k + 1) << 16, (2 * k + 2) << 16
@@ -112,11 +149,16 @@ def heap_bvh(n_leaves):
     return rec.tobytes()
 
 
-@pytest.mark.parametrize("n_leaves,ok", [(1024, True), (1025, False)])
-def test_link_format_needs_16_bit_offsets(n_leaves, ok):
-    # 2 n_leaves - 1 threaded nodes; offsets of 32 B nodes fit 16 bits up to 2047 nodes
-    L = rtamd.amd()
+@pytest.mark.parametrize("n_leaves", [1024, 1025, 4096, 32768])
+def test_link_format_reaches_the_16_bit_node_limit(n_leaves):
+    """Up to 2 * 32768 - 1 = 65535 nodes (the reference's 16-bit node indices)."""
     b = heap_bvh(n_leaves)
-    n = ctypes.c_int(-1)
-    assert L.rt_debug_link_nodes(ctypes.create_string_buffer(b, len(b)), len(b), None, 0, ctypes.byref(n)) == 0
-    assert (n.value > 0) == ok
+    tn = threaded_of(b)
+    ln = links_of(b)
+    assert len(tn) == 2 * n_leaves - 1 and len(ln) > 0
+    order = check_layout(tn, ln)
+    if n_leaves <= 4096:
+        rng = np.random.default_rng(n_leaves)
+        for p in (0.5, 0.9, 1.0):
+            hits = rng.random(len(tn)) < p
+            assert walk_links(ln, len(tn), hits, order) == walk_threaded(tn, hits)

@@ -10,6 +10,8 @@ usage: python tools/ab_variants.py [--variants 30c0,30c16] [--rounds 5] [--scene
 """
 import argparse
 import os
+
+os.environ.setdefault("RTAMD_LIB", "ab")   # the A/B build reads the RT_* knobs (rtamd._lib.amd)
 import statistics
 import sys
 

@@ -18,7 +18,7 @@ run() {   # name timeout cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q --maxfail=25 -rf --durations=20 --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     ab)    run ab 600 python tools/ab_variants.py ${AB_ARGS:-} ;;
