@@ -48,8 +48,9 @@ typedef struct rt_ctx rt_ctx;
 
 /* Create a context rendering on n_devices HIP devices (device_ids may be NULL
  * for 0..n-1; explicit ids may repeat, n <= 64).  Rows are split in
- * interleaved stripes over the device slots and gathered on the host by
- * rt_read_image; the result equals a 1-device render bit for bit.
+ * interleaved stripes over the device slots and gathered on device 0 by
+ * rt_read_image (RCCL, see rt_comm_*); the result equals a 1-device render bit
+ * for bit.
  * Replaces: Window.initGLFW/initShaderPrograms (Window.java:90-193). */
 int rt_create(int n_devices, const int* device_ids, rt_ctx** out);
 int rt_destroy(rt_ctx* ctx);
@@ -105,6 +106,12 @@ int rt_write_image(rt_ctx* ctx, const float* rgba);
  * Replaces: QueryTimer GL_TIME_ELAPSED (QueryTimer.java:24-50). */
 int rt_last_render_ns(rt_ctx* ctx, uint64_t* ns);
 
+/* Non-blocking: returns 1 with *ns (max over devices) once the last rt_render
+ * call has finished on the device, 0 while it still runs (*ns untouched).
+ * Replaces: the polling of finished QueryTimer results that feeds
+ * lastDispatchTime on every raytrace() (RaytraceExecutor.java:106-115). */
+int rt_render_done(rt_ctx* ctx, uint64_t* ns);
+
 /* ---- MI355X-native extensions (no reference counterpart) ---------------- */
 
 /* Multi-process partition (one process per GPU): this context renders only the
@@ -122,6 +129,25 @@ int rt_bind_device_image(rt_ctx* ctx, void* device_ptr, size_t nbytes);
 
 /* Use a caller-provided hipStream_t (e.g. torch's current stream); NULL = own. */
 int rt_set_stream(rt_ctx* ctx, void* hip_stream);
+
+/* ---- RCCL over xGMI behind the ABI (the partition's one exchange).
+ * A context over several devices (rt_create(n > 1)) gathers in rt_read_image: each
+ * device's stripe block to device 0 over RCCL (ncclCommInitAll; one ncclSend /
+ * ncclRecv pair per device) when the device ids are distinct, else by peer copies,
+ * then a de-interleave kernel on device 0 and one copy to the host.
+ * One process per GPU: rank 0 makes a communicator id (RT_COMM_ID_BYTES bytes) that
+ * the host hands to every rank by its own means (the reference has no transport);
+ * each rank, after rt_set_partition(rank, world, ...), calls rt_comm_init; then
+ * rt_gather_image sends every rank's stripe block to rank 0 over RCCL, where it is
+ * de-interleaved on the device and copied out (rgba: W*H*4 floats on rank 0, NULL
+ * elsewhere).  librccl.so is loaded on first use. */
+#define RT_COMM_ID_BYTES 128
+enum { RT_GATHER_HOST = 0, RT_GATHER_PEER = 1, RT_GATHER_RCCL = 2 };
+int rt_comm_unique_id(void* id_out);
+int rt_comm_init(rt_ctx* ctx, const void* id, int rank, int world);
+int rt_gather_image(rt_ctx* ctx, float* rgba);
+/* How the last gather ran: RT_GATHER_*, or -1 before any. */
+int rt_gather_path(rt_ctx* ctx);
 
 /* Host helper: scatter gathered stripe blocks [world][padded_rows][W][4] into a
  * full W x H image (row 0 = top). */

@@ -36,6 +36,11 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
  * there is no BVH. */
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4);
 
+/* Host-only: rt_read_image's device de-interleave (deinterleave_kernel) with the same
+ * row indexing (rt_device.h rt_gathered_row), on the host (tests compare it with
+ * rt_deinterleave_rows). */
+int rt_debug_deinterleave(const float* gathered, int width, int height, int world, int stripe_rows, float* out);
+
 /* Host-only: the boxes' 48-byte records rt_upload_buffer(RT_BIND_BOXES) builds
  * (rt_capi.hip box_record: 3 float4 per box; float4[2].y = 1 for a compact record,
  * whose faces the kernel rebuilds from it) and how many are compact. */

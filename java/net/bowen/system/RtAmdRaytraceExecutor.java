@@ -9,7 +9,7 @@ import java.util.concurrent.TimeUnit;
  * instead of OpenGL: the same public methods, the same per-frame uniforms
  * (frame_count = ++numSamples, u_rand_factor = (float) Math.random(), :124-127) and
  * the same completion bookkeeping, with the dispatch, the memory barrier and the
- * GL_TIME_ELAPSED query replaced by rt_render / rt_last_render_ns.
+ * GL_TIME_ELAPSED query replaced by rt_render / rt_render_done / rt_last_render_ns.
  *
  * <p>Drop-in: Window.initRaytraceExecutor constructs this instead of
  * {@code new RaytraceExecutor(quadTexture, program)}; the frame loop
@@ -81,7 +81,10 @@ public class RtAmdRaytraceExecutor {
         return sb.append(seconds).append('.').append(finishTime % 1000).append("seconds").toString();
     }
 
-    /** Milliseconds of the last rt_render call (the reference truncates its timer query to int ms). */
+    /**
+     * Milliseconds of the last finished rt_render call (the reference truncates its timer
+     * query to int ms), refreshed by every raytrace() as the GUI status line expects.
+     */
     public int getLastDispatchTime() {
         return lastDispatchTime;
     }
@@ -99,6 +102,12 @@ public class RtAmdRaytraceExecutor {
     public void raytrace(int n) {
         if (n <= 0) return;
         if (numSamples == 0) startMillis = System.currentTimeMillis();
+        // as the reference does with its finished QueryTimers (RaytraceExecutor.java:106-115): the
+        // previous call's device time once it is available, never waiting for it
+        if (numSamples > 0) {
+            long ns = rt.renderDoneNanos();
+            if (ns >= 0) lastDispatchTime = (int) (ns / 1_000_000L);
+        }
         float[] factors = new float[n];
         for (int i = 0; i < n; i++) factors[i] = (float) Math.random();
         rt.render(numSamples + 1, factors);

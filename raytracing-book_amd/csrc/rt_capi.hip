@@ -17,12 +17,48 @@
 #include <string>
 #include <vector>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>   // types only: librccl (~570 MB) is dlopen'ed by the first gather that uses it
+
 #include "rt/rt.h"
 #include "rt/rt_debug.h"
 #include "rt/rt_types.h"
 #include "rt_device.h"
 
 namespace {
+
+// RCCL, loaded on first use (rt_comm_*, multi-device rt_read_image).  Not linked: a
+// single-device context never pays for loading it.
+struct Rccl {
+    bool tried = false, ok = false;
+    void* h = nullptr;
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommInitAll) CommInitAll = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclSend) Send = nullptr;
+    decltype(&ncclRecv) Recv = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+};
+Rccl& rccl() {
+    static Rccl r;
+    if (!r.tried) {
+        r.tried = true;
+        r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!r.h) r.h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (r.h) {
+#define RT_SYM(F) r.F = reinterpret_cast<decltype(r.F)>(dlsym(r.h, "nccl" #F))
+            RT_SYM(GetUniqueId); RT_SYM(CommInitRank); RT_SYM(CommInitAll); RT_SYM(CommDestroy); RT_SYM(Send);
+            RT_SYM(Recv); RT_SYM(GroupStart); RT_SYM(GroupEnd); RT_SYM(GetErrorString);
+#undef RT_SYM
+            r.ok = r.GetUniqueId && r.CommInitRank && r.CommInitAll && r.CommDestroy && r.Send && r.Recv &&
+                   r.GroupStart && r.GroupEnd && r.GetErrorString;
+        }
+    }
+    return r;
+}
 
 struct DevBuf {
     void* ptr = nullptr;
@@ -57,6 +93,8 @@ struct Device {
     bool image_bound = false;
     int rank = 0, world = 1;     // stripe assignment of this device
     int local_rows = 0, padded_rows = 0;
+    ncclComm_t comm = nullptr;   // RCCL communicator of a device gather (rank = this device's slot / process rank)
+    DevBuf gather, full;         // device 0 / rank 0: the gathered stripe blocks, the de-interleaved image
 };
 
 // Tables of the exact near-first walk (build_fast below; rt_kernel.hip trace_fast).
@@ -137,6 +175,10 @@ struct rt_ctx {
     size_t sample_budget = (size_t)32 << 30;   // staged colours per launch, at most (and at most half the free memory)
     int last_launch[RT_LI_N] = {0};
     bool launched = false;
+    // gathers (rt_read_image of a multi-device context, rt_gather_image): RT_GATHER_*
+    int gather_path = -1;
+    bool comm_tried = false;     // ncclCommInitAll of a multi-device context attempted
+    bool proc_comm = false;      // rt_comm_init: one rank of a multi-process communicator
 };
 
 namespace {
@@ -847,11 +889,164 @@ int alloc_image(rt_ctx* c, Device& d) {
     return RT_OK;
 }
 
+int ensure(rt_ctx* c, Device& d, DevBuf& b, size_t n) {
+    if (b.bytes >= n) return RT_OK;
+    dev_free(b);
+    HIPCHK(c, hipSetDevice(d.id));
+    HIPCHK(c, hipMalloc(&b.ptr, n));
+    b.bytes = n;
+    return RT_OK;
+}
+
+#define NCCLCHK(ctx, call)                                                                               \
+    do {                                                                                                 \
+        ncclResult_t e_ = (call);                                                                        \
+        if (e_ != ncclSuccess)                                                                           \
+            return set_err(ctx, RT_ERR_DEVICE, std::string(#call) + ": " + rccl().GetErrorString(e_));    \
+    } while (0)
+
+// Multi-device context: device k's stripe block (local_rows x W, in its padded slot) into
+// device 0's gather buffer, then the de-interleave kernel into device 0's full image.
+// RCCL (ncclCommInitAll over the context's devices, one ncclSend per device k > 0 and the
+// matching ncclRecv on device 0, grouped) when the device ids are distinct and RCCL
+// loads; peer copies otherwise (several slots on one device: RCCL allows one rank per
+// device).  The renders were synchronised by the caller.
+int device_gather(rt_ctx* c) {
+    const int ndev = (int)c->devs.size();
+    const int padded = padded_rows_of(c->height, ndev, c->stripe_rows);
+    const size_t slot = (size_t)padded * c->width * 16;
+    Device& d0 = c->devs[0];
+    if (ensure(c, d0, d0.gather, slot * ndev) || ensure(c, d0, d0.full, (size_t)c->height * c->width * 16))
+        return RT_ERR_DEVICE;
+    if (!c->comm_tried) {
+        c->comm_tried = true;
+        bool distinct = true;
+        for (int i = 0; i < ndev; i++)
+            for (int j = 0; j < i; j++) distinct = distinct && c->devs[i].id != c->devs[j].id;
+        if (distinct && rccl().ok) {
+            std::vector<ncclComm_t> comms(ndev, nullptr);
+            std::vector<int> ids(ndev);
+            for (int k = 0; k < ndev; k++) ids[k] = c->devs[k].id;
+            if (rccl().CommInitAll(comms.data(), ndev, ids.data()) == ncclSuccess)
+                for (int k = 0; k < ndev; k++) c->devs[k].comm = comms[k];
+        }
+    }
+    if (d0.comm) {
+        NCCLCHK(c, rccl().GroupStart());
+        for (int k = 0; k < ndev; k++) {
+            Device& d = c->devs[k];
+            const size_t n = (size_t)d.local_rows * c->width * 4;   // floats of the block
+            char* dst = (char*)d0.gather.ptr + slot * k;
+            HIPCHK(c, hipSetDevice(d.id));
+            if (k == 0) {
+                HIPCHK(c, hipMemcpyAsync(dst, d.image_ptr, n * 4, hipMemcpyDeviceToDevice, d0.stream));
+            } else if (n) {
+                NCCLCHK(c, rccl().Send(d.image_ptr, n, ncclFloat, 0, d.comm, d.stream));
+                NCCLCHK(c, rccl().Recv(dst, n, ncclFloat, k, d0.comm, d0.stream));
+            }
+        }
+        NCCLCHK(c, rccl().GroupEnd());
+        for (Device& d : c->devs) {
+            HIPCHK(c, hipSetDevice(d.id));
+            HIPCHK(c, hipStreamSynchronize(d.stream));
+        }
+        c->gather_path = RT_GATHER_RCCL;
+    } else {
+        HIPCHK(c, hipSetDevice(d0.id));
+        for (int k = 0; k < ndev; k++) {
+            Device& d = c->devs[k];
+            HIPCHK(c, hipMemcpyPeerAsync((char*)d0.gather.ptr + slot * k, d0.id, d.image_ptr, d.id,
+                                         (size_t)d.local_rows * c->width * 16, d0.stream));
+        }
+        c->gather_path = RT_GATHER_PEER;
+    }
+    HIPCHK(c, hipSetDevice(d0.id));
+    if (rt_launch_deinterleave(d0.gather.ptr, d0.full.ptr, c->width, c->height, ndev, c->stripe_rows, padded,
+                               d0.stream))
+        return set_err(c, RT_ERR_DEVICE, "de-interleave kernel launch failed");
+    HIPCHK(c, hipStreamSynchronize(d0.stream));
+    return RT_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+// ---- one process per GPU: RCCL behind the ABI (rt.h rt_comm_*) ----------------
+int rt_comm_unique_id(void* id_out) {
+    if (!id_out) return RT_ERR_INVALID_ARG;
+    if (!rccl().ok) return RT_ERR_DEVICE;
+    ncclUniqueId id;
+    if (rccl().GetUniqueId(&id) != ncclSuccess) return RT_ERR_DEVICE;
+    static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "ncclUniqueId is 128 bytes");
+    std::memcpy(id_out, &id, sizeof(id));
+    return RT_OK;
+}
+
+int rt_comm_init(rt_ctx* c, const void* id, int rank, int world) {
+    if (!c || !id) return RT_ERR_INVALID_ARG;
+    if (c->devs.size() != 1) return set_err(c, RT_ERR_STATE, "rt_comm_init needs a 1-device context");
+    if (world != c->proc_world || rank != c->proc_rank)
+        return set_err(c, RT_ERR_STATE, "rt_comm_init: rank / world differ from rt_set_partition's");
+    if (!rccl().ok) return set_err(c, RT_ERR_DEVICE, "RCCL (librccl.so) could not be loaded");
+    Device& d = c->devs[0];
+    HIPCHK(c, hipSetDevice(d.id));
+    if (d.comm) {
+        (void)rccl().CommDestroy(d.comm);
+        d.comm = nullptr;
+    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    NCCLCHK(c, rccl().CommInitRank(&d.comm, world, uid, rank));
+    c->proc_comm = true;
+    return RT_OK;
+}
+
+int rt_gather_image(rt_ctx* c, float* rgba) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (c->width <= 0) return set_err(c, RT_ERR_STATE, "no image");
+    if (c->devs.size() != 1) {   // a multi-device context gathers in rt_read_image
+        if (!rgba) return set_err(c, RT_ERR_INVALID_ARG, "NULL image");
+        return rt_read_image(c, rgba);
+    }
+    Device& d = c->devs[0];
+    if (!c->proc_comm || !d.comm) return set_err(c, RT_ERR_STATE, "rt_comm_init before rt_gather_image");
+    if (c->proc_rank == 0 && !rgba) return set_err(c, RT_ERR_INVALID_ARG, "rank 0 needs the output image");
+    int r = rt_sync(c);
+    if (r) return r;
+    HIPCHK(c, hipSetDevice(d.id));
+    const int world = c->proc_world;
+    // rank k sends its local_rows x W block (a bound image holds no more); rank 0 receives
+    // it into slot k of the padded gather buffer
+    const size_t slot = (size_t)d.padded_rows * c->width * 16;
+    if (c->proc_rank == 0) {
+        if (ensure(c, d, d.gather, slot * world) || ensure(c, d, d.full, (size_t)c->height * c->width * 16))
+            return RT_ERR_DEVICE;
+        NCCLCHK(c, rccl().GroupStart());
+        HIPCHK(c, hipMemcpyAsync(d.gather.ptr, d.image_ptr, (size_t)d.local_rows * c->width * 16,
+                                 hipMemcpyDeviceToDevice, d.stream));
+        for (int k = 1; k < world; k++) {
+            const size_t nk = (size_t)local_rows_of(c->height, k, world, c->stripe_rows) * c->width * 4;
+            if (nk) NCCLCHK(c, rccl().Recv((char*)d.gather.ptr + slot * k, nk, ncclFloat, k, d.comm, d.stream));
+        }
+        NCCLCHK(c, rccl().GroupEnd());
+        if (rt_launch_deinterleave(d.gather.ptr, d.full.ptr, c->width, c->height, world, c->stripe_rows,
+                                   d.padded_rows, d.stream))
+            return set_err(c, RT_ERR_DEVICE, "de-interleave kernel launch failed");
+        int r2 = d2h(c, d, rgba, d.full.ptr, (size_t)c->height * c->width * 16);
+        if (r2) return r2;
+    } else {
+        const size_t n = (size_t)d.local_rows * c->width * 4;
+        if (n) NCCLCHK(c, rccl().Send(d.image_ptr, n, ncclFloat, 0, d.comm, d.stream));
+        HIPCHK(c, hipStreamSynchronize(d.stream));
+    }
+    c->gather_path = RT_GATHER_RCCL;
+    return RT_OK;
+}
+
+int rt_gather_path(rt_ctx* c) { return c ? c->gather_path : RT_ERR_INVALID_ARG; }
 
 // Failure of the last context-less call (rt_create) on this thread; rt_last_error(NULL).
 namespace { thread_local std::string g_create_err; }
@@ -918,6 +1113,8 @@ int rt_destroy(rt_ctx* c) {
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter);
         dev_free(d.tile_done); dev_free(d.samples); dev_free(d.wbuf); dev_free(d.dquads); dev_free(d.dboxes);
         dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links); dev_free(d.dboxc);
+        dev_free(d.gather); dev_free(d.full);
+        if (d.comm && rccl().ok) (void)rccl().CommDestroy(d.comm);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)
             if (e) (void)hipEventDestroy(e);
@@ -1502,6 +1699,23 @@ int rt_last_render_ns(rt_ctx* c, uint64_t* ns) {
     return RT_OK;
 }
 
+int rt_render_done(rt_ctx* c, uint64_t* ns) {
+    if (!c || !ns) return RT_ERR_INVALID_ARG;
+    double mx = 0;
+    for (Device& d : c->devs) {
+        if (!d.timed) continue;
+        HIPCHK(c, hipSetDevice(d.id));
+        const hipError_t q = hipEventQuery(d.ev_stop);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return set_err(c, RT_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(q));
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, d.ev_start, d.ev_stop));
+        mx = std::max(mx, (double)ms);
+    }
+    *ns = (uint64_t)(mx * 1e6);
+    return 1;
+}
+
 int rt_read_image(rt_ctx* c, float* rgba) {
     if (!c || !rgba) return RT_ERR_INVALID_ARG;
     if (c->width <= 0) return set_err(c, RT_ERR_STATE, "no image");
@@ -1512,7 +1726,14 @@ int rt_read_image(rt_ctx* c, float* rgba) {
         HIPCHK(c, hipSetDevice(d.id));
         return d2h(c, d, rgba, d.image_ptr, (size_t)d.local_rows * c->width * 16);
     }
-    // multi-device context: gather stripes to the host and de-interleave
+    // multi-device context: the stripe blocks gathered on device 0 (RCCL when the devices
+    // are distinct and RCCL loads, else peer copies), de-interleaved there, one copy out
+    if (device_gather(c) == RT_OK) {
+        Device& d0 = c->devs[0];
+        HIPCHK(c, hipSetDevice(d0.id));
+        return d2h(c, d0, rgba, d0.full.ptr, (size_t)c->height * c->width * 16);
+    }
+    // last resort: every block to the host, de-interleaved there
     int ndev = (int)c->devs.size();
     int padded = padded_rows_of(c->height, ndev, c->stripe_rows);
     std::vector<float> g((size_t)ndev * padded * c->width * 4, 0.0f);
@@ -1523,6 +1744,7 @@ int rt_read_image(rt_ctx* c, float* rgba) {
                      (size_t)d.local_rows * c->width * 16);
         if (r2) return r2;
     }
+    c->gather_path = RT_GATHER_HOST;
     return rt_deinterleave_rows(g.data(), c->width, c->height, ndev, c->stripe_rows, rgba);
 }
 
@@ -1603,6 +1825,17 @@ int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t ou
     if (out) {
         if (out_cap < dn.size() * sizeof(rt_dnode)) return RT_ERR_INVALID_ARG;
         std::memcpy(out, dn.data(), dn.size() * sizeof(rt_dnode));
+    }
+    return RT_OK;
+}
+
+int rt_debug_deinterleave(const float* gathered, int width, int height, int world, int stripe_rows, float* out) {
+    if (!gathered || !out || width <= 0 || height <= 0 || world < 1 || stripe_rows < 1) return RT_ERR_INVALID_ARG;
+    const int padded = padded_rows_of(height, world, stripe_rows);
+    for (int y = 0; y < height; y++) {   // deinterleave_kernel's indexing, one row at a time
+        int k, lr;
+        rt_gathered_row(y, world, stripe_rows, &k, &lr);
+        std::memcpy(out + (size_t)y * width * 4, gathered + ((size_t)k * padded + lr) * width * 4, (size_t)width * 16);
     }
     return RT_OK;
 }

@@ -172,5 +172,16 @@ enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)
 // sets a.acc_lds; info (may be NULL): RT_LI_* of the launch
 int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int* info);
+// Row y of the image in the gathered stripe blocks [world][padded_rows][W]: rank k = s % world
+// of its stripe s = y / stripe_rows, local row (s / world) * stripe_rows + y % stripe_rows
+// (rt_set_partition).  Shared by deinterleave_kernel and rt_debug_deinterleave.
+__host__ __device__ inline void rt_gathered_row(int y, int world, int stripe_rows, int* k, int* lr) {
+    const int s = y / stripe_rows;
+    *k = s % world;
+    *lr = (s / world) * stripe_rows + y % stripe_rows;
+}
+// gathered stripe blocks [world][padded_rows][W] float4 -> [H][W] float4 (device 0 of a gather)
+int rt_launch_deinterleave(const void* gathered, void* out, int width, int height, int world, int stripe_rows,
+                           int padded_rows, void* stream);
 // debug: evaluate GLSL built-ins on device (tests)
 int rt_launch_eval_builtin(int fn, const float* dx, const float* dy, float* dout, int n, void* stream);

@@ -2122,6 +2122,20 @@ __global__ void __launch_bounds__(256) fold_kernel(const KP* __restrict__ Pp) {
     *px = prev;
 }
 
+// Gathered stripe blocks [world][padded_rows][W] float4 -> the image [H][W] (row 0 = top):
+// row y belongs to stripe s = y / stripe_rows, rendered by rank s % world as its local row
+// (s / world) * stripe_rows + y % stripe_rows (rt_set_partition).  One thread per pixel,
+// coalesced along the row on both sides.
+__global__ void __launch_bounds__(256) deinterleave_kernel(const float4* __restrict__ g, float4* __restrict__ out,
+                                                           int width, int height, int world, int stripe_rows,
+                                                           int padded_rows) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= width || y >= height) return;
+    int k, lr;
+    rt_gathered_row(y, world, stripe_rows, &k, &lr);
+    out[(size_t)y * width + x] = g[((size_t)k * padded_rows + lr) * width + x];
+}
+
 __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const float* __restrict__ y,
                                     float* __restrict__ out, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2285,6 +2299,15 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         const unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);
         hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), 0, st, d);
     }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int rt_launch_deinterleave(const void* gathered, void* out, int width, int height, int world, int stripe_rows,
+                           int padded_rows, void* stream) {
+    if (width <= 0 || height <= 0) return 0;
+    hipLaunchKernelGGL(deinterleave_kernel, dim3((unsigned)((width + 255) / 256), (unsigned)height), dim3(256), 0,
+                       (hipStream_t)stream, (const float4*)gathered, (float4*)out, width, height, world, stripe_rows,
+                       padded_rows);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

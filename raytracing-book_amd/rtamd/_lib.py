@@ -80,6 +80,7 @@ def _amd_protos(L):
     _proto(L, "rt_read_image", i, vp, c_float_p)
     _proto(L, "rt_write_image", i, vp, c_float_p)
     _proto(L, "rt_last_render_ns", i, vp, ctypes.POINTER(u64))
+    _proto(L, "rt_render_done", i, vp, ctypes.POINTER(u64))
     _proto(L, "rt_set_partition", i, vp, i, i, i)
     _proto(L, "rt_local_rows", i, i, i, i, i)
     _proto(L, "rt_padded_local_rows", i, i, i, i)
@@ -87,12 +88,17 @@ def _amd_protos(L):
     _proto(L, "rt_set_stream", i, vp, vp)
     _proto(L, "rt_deinterleave_rows", i, c_float_p, i, i, i, i, c_float_p)
     _proto(L, "rt_frame_rand_factor", f, u64, u64)
+    _proto(L, "rt_comm_unique_id", i, vp)
+    _proto(L, "rt_comm_init", i, vp, vp, i, i)
+    _proto(L, "rt_gather_image", i, vp, c_float_p)
+    _proto(L, "rt_gather_path", i, vp)
     _proto(L, "rt_debug_eval_builtin", i, i, i, c_float_p, c_float_p, c_float_p, i)
     _proto(L, "rt_debug_threaded_bvh", i, vp, sz, vp, sz, c_int_p)
     _proto(L, "rt_debug_fast_tables", i, vp, sz, vp, sz, vp, sz, i, vp, sz, c_int_p,
            ctypes.POINTER(ctypes.c_uint32), sz, c_int_p, c_int_p)
     _proto(L, "rt_debug_link_nodes", i, vp, sz, vp, sz, c_int_p)
     _proto(L, "rt_debug_box_records", i, vp, sz, vp, sz, c_int_p)
+    _proto(L, "rt_debug_deinterleave", i, c_float_p, i, i, i, i, c_float_p)
     _proto(L, "rt_debug_device_count", i)
     _proto(L, "rt_debug_enable_stats", i, vp, i)
     _proto(L, "rt_debug_read_stats", i, vp, ctypes.POINTER(ctypes.c_ulonglong), i)

@@ -55,3 +55,17 @@ def gather_image(local_block, height, world, stripe_rows):
         return deinterleave(g, height, world, stripe_rows)
     dist.gather(blk, dst=0)
     return None
+
+
+def native_gather(ctx, rank, world):
+    """The gather through the C ABI (rt_comm_init + rt_gather_image: RCCL sends to rank 0,
+    de-interleave kernel there): rank 0 makes the communicator id, torch.distributed
+    hands it to the other ranks (the only use of torch.distributed here).  Returns the
+    [H, W, 4] image on rank 0, None elsewhere."""
+    from .render import comm_unique_id
+    if world == 1:
+        return ctx.read_image()
+    box = [comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    ctx.comm_init(box[0], rank, world)
+    return ctx.gather_image()

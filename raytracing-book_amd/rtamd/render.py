@@ -33,6 +33,17 @@ def frame_rand_factors(seed, start, n):
     return out
 
 
+def comm_unique_id(lib=None):
+    """rt_comm_unique_id: a fresh 128-byte RCCL communicator id (rank 0 makes it, the host
+    hands it to every rank)."""
+    L = lib or _lib.amd()
+    buf = ctypes.create_string_buffer(128)
+    rc = L.rt_comm_unique_id(buf)
+    if rc != 0:
+        raise RTError(rc, "rt_comm_unique_id failed (RCCL unavailable)")
+    return buf.raw
+
+
 def local_rows(height, rank, world, stripe_rows):
     n_stripes = (height + stripe_rows - 1) // stripe_rows
     return sum(min(stripe_rows, height - s * stripe_rows) for s in range(rank, n_stripes, world))
@@ -180,6 +191,14 @@ class RenderContext:
         self._check(self._L.rt_last_render_ns(self._h, ctypes.byref(v)))
         return v.value
 
+    def render_done(self):
+        """rt_render_done: the last render's device ns once it finished, else None (no wait)."""
+        v = ctypes.c_uint64()
+        rc = self._L.rt_render_done(self._h, ctypes.byref(v))
+        if rc < 0:
+            self._check(rc)
+        return v.value if rc == 1 else None
+
     def read_image(self):
         """[local_rows, W, 4] float32 (the full image for an unpartitioned context)."""
         out = np.empty((self.local_rows, self.width, 4), dtype=np.float32)
@@ -189,6 +208,25 @@ class RenderContext:
     def write_image(self, rgba):
         rgba = np.ascontiguousarray(rgba, dtype=np.float32)
         self._check(self._L.rt_write_image(self._h, rgba.ctypes.data_as(c_float_p)))
+
+    # -- RCCL behind the ABI (rt.h rt_comm_*): one process per GPU
+    def comm_init(self, uid, rank, world):
+        """rt_comm_init with the 128-byte id rank 0 made (comm_unique_id)."""
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        self._check(self._L.rt_comm_init(self._h, buf, int(rank), int(world)))
+
+    def gather_image(self):
+        """rt_gather_image: the full [H, W, 4] image on rank 0 (None on the other ranks)."""
+        if self.rank == 0:
+            out = np.empty((self.height, self.width, 4), dtype=np.float32)
+            self._check(self._L.rt_gather_image(self._h, out.ctypes.data_as(c_float_p)))
+            return out
+        self._check(self._L.rt_gather_image(self._h, None))
+        return None
+
+    def gather_path(self):
+        """How the last gather ran: 'host', 'peer' (device copies) or 'rccl' (None before any)."""
+        return {0: "host", 1: "peer", 2: "rccl"}.get(self._L.rt_gather_path(self._h))
 
     def bind_device_image(self, ptr, nbytes):
         self._check(self._L.rt_bind_device_image(self._h, ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes)))
@@ -257,6 +295,10 @@ class RaytraceExecutor:
     def raytrace(self, n_frames=1):              # :100-142
         if self.numSamples == 0:
             self._start = time.time()
+        # the previous call's device time once it is available, without waiting (:106-115)
+        done = self.ctx.render_done() if self.numSamples else None
+        if done is not None:
+            self.lastDispatchTime = done // 1_000_000
         n = max(0, min(int(n_frames), self.samplePerPixel - self.numSamples)) if self.samplePerPixel else int(n_frames)
         if n == 0:
             return

@@ -101,7 +101,8 @@ def test_stripe_arithmetic():
                 assert total == H and sorted(owned) == list(range(H))
 
 
-@pytest.mark.parametrize("H,W,world,stripe", [(37, 5, 3, 4), (1080, 3, 8, 16), (9, 2, 2, 16)])
+@pytest.mark.parametrize("H,W,world,stripe", [(37, 5, 3, 4), (1080, 3, 8, 16), (9, 2, 2, 16), (2160, 2, 8, 8),
+                                              (45, 4, 5, 64), (7, 3, 8, 1)])
 def test_deinterleave_matches(H, W, world, stripe):
     L = rtamd.amd()
     padded = rtamd.padded_local_rows(H, world, stripe)
@@ -110,6 +111,10 @@ def test_deinterleave_matches(H, W, world, stripe):
     fp = lambda a: a.ctypes.data_as(_lib.c_float_p)  # noqa: E731
     assert L.rt_deinterleave_rows(fp(g), W, H, world, stripe, fp(out)) == 0
     assert np.array_equal(out, rtamd.deinterleave(g, H, world, stripe))
+    # the device gather's indexing (deinterleave_kernel / rt_gathered_row), run on the host
+    dev = np.zeros((H, W, 4), np.float32)
+    assert L.rt_debug_deinterleave(fp(g), W, H, world, stripe, fp(dev)) == 0
+    assert np.array_equal(dev, out)
 
 
 # --- threaded BVH == the reference's stack traversal order --------------------------------------

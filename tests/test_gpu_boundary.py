@@ -59,13 +59,42 @@ def test_stripe_partition_contexts(gpu, world, stripe):
     assert bit_equal(img, full), mismatch_report(img, full)
 
 
-def test_multi_device_context_host_gather(gpu):
-    """A context over several device slots (here device 0 twice) splits rows in stripes
-    and gathers on the host; equals the single-slot render."""
+@pytest.mark.parametrize("devices", [(0, 0), (0, 0, 0)])
+def test_multi_device_context_device_gather(gpu, devices):
+    """A context over several device slots (here device 0 repeated) splits rows in stripes;
+    rt_read_image gathers the blocks on device 0 (peer copies: RCCL allows one rank per
+    device) and de-interleaves them there; equals the single-slot render."""
     s = rtamd.Scene(6, 40, 37, seed=1)
     a = gpu_image(s, 4)
-    b = gpu_image(s, 4, devices=(0, 0))
+    ctx = rtamd.RenderContext(devices=devices)
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=4)
+    ctx.resize(40, 37)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+    b = ctx.read_image()
+    assert ctx.gather_path() == "peer"
+    ctx.close()
     assert bit_equal(a, b), mismatch_report(a, b)
+
+
+def test_process_communicator_gather(gpu):
+    """rt_comm_unique_id / rt_comm_init / rt_gather_image: the RCCL path a one-process-per-GPU
+    host takes without any Python harness, here as a world-1 communicator on one GPU (the
+    N-rank sends are unmeasured on this one-GPU box)."""
+    s = rtamd.Scene(8, 48, 27, seed=1)
+    ref = oracle_image(s, 3)
+    ctx = rtamd.RenderContext()
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=3)
+    ctx.resize(48, 27)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 3))
+    with pytest.raises(rtamd.RTError, match="rt_comm_init"):
+        ctx.gather_image()
+    ctx.comm_init(rtamd.comm_unique_id(), 0, 1)
+    out = ctx.gather_image()
+    assert ctx.gather_path() == "rccl"
+    ctx.close()
+    assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
 @pytest.mark.parametrize("w,h", [(1, 1), (7, 3), (65, 9), (3, 70), (129, 1)])
