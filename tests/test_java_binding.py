@@ -65,3 +65,89 @@ def test_executor_mirror_keeps_the_reference_methods():
                 "int getLastDispatchTime()", "void addCompleteListener(Runnable", "void raytrace()",
                 "boolean sampleComplete()"]:
         assert f"public {sig}" in src, sig
+
+
+PATCH = os.path.join(REPO, "java", "patches", "rtamd-dropin.patch")
+
+
+def _patch_files():
+    files, cur = {}, None
+    for line in open(PATCH):
+        if line.startswith("+++ "):
+            cur = line.split()[1].split("/src/main/java/", 1)[1]
+            files[cur] = {"+": [], "-": []}
+        elif cur and line[:1] in "+-" and not line.startswith(("+++", "---")):
+            files[cur][line[0]].append(line[1:].rstrip("\n"))
+    return files
+
+
+def test_dropin_patch_replaces_every_gl_call_site():
+    """java/patches/rtamd-dropin.patch (against the reference tree) switches each hot-path
+    GL call site of SURVEY §8b to the C ABI: the six SSBO uploads of RaytraceModel.put*ToProgram
+    (RaytraceModel.java:115-246), Texture.putData's glTexImage2D and putTextureIndices
+    (Texture.java:122-133, 238-247), Camera.putToShaderProgram's UBO + background uniform
+    (Camera.java:121-143), Window.initRaytraceExecutor / saveImage / resize / loop
+    (Window.java:116-129, 213-238, 250-281) and GuiRenderer.maxDepthUpdate (GuiRenderer.java:64-68)."""
+    f = _patch_files()
+    rm = f["net/bowen/draw/models/raytrace/RaytraceModel.java"]
+    for ssbo, binding in [("sphereSSBO", "SPHERES"), ("quadSSBO", "QUADS"), ("boxesSSBO", "BOXES"),
+                          ("constantMediumSSBO", "MEDIA"), ("bvhSSBO", "BVH"), ("lightsSSBO", "LIGHTS")]:
+        assert any(f"{ssbo}.uploadData(buffer, GL_STATIC_DRAW);" in l for l in rm["-"]), ssbo
+        assert any(f"RtAmdBackend.upload(RtAmd.{binding}, buffer);" in l for l in rm["+"]), binding
+    tx = f["net/bowen/draw/textures/Texture.java"]
+    assert sum("RtAmdBackend.putTexture(this, internalFormat, format, type, width, height, data);" in l
+               for l in tx["+"]) == 2
+    assert any("RtAmdBackend.uploadTextures(TEXTURES_IN_COMPUTE);" in l for l in tx["+"])
+    cam = f["net/bowen/draw/models/raytrace/Camera.java"]
+    assert any("ubo.uploadData(buffer, GL_STATIC_DRAW);" in l for l in cam["-"])
+    assert any('setUniform3fv("background"' in l for l in cam["-"])
+    assert any("RtAmdBackend.setCamera(buffer, background.asArray());" in l for l in cam["+"])
+    win = f["net/bowen/gui/Window.java"]
+    assert any("new RaytraceExecutor(screenQuadTexture, computeProgram)" in l for l in win["-"])
+    assert any("new RtAmdRaytraceExecutor(RtAmdBackend.get())" in l for l in win["+"])
+    assert any("screenQuadTexture.saveAsPNG(outputFile);" in l for l in win["-"])
+    assert any("RtAmdBackend.saveAsPNG(outputFile)" in l for l in win["+"])
+    assert any("RtAmdBackend.get().resize(width, height);" in l for l in win["+"])
+    gui = f["net/bowen/gui/GuiRenderer.java"]
+    assert any('setUniform1iv("max_depth"' in l for l in gui["-"])
+    assert any("raytraceExecutor.setMaxDepth(maxDepth[0]);" in l for l in gui["+"])
+
+
+def _methods(java_file):
+    src = open(os.path.join(JAVA, java_file)).read()
+    return set(re.findall(r"public (?:static )?(?:synchronized )?[\w\[\]<>]+ (\w+)\(", src)), src
+
+
+def test_dropin_calls_resolve_to_the_binding():
+    """Every RtAmdBackend / RtAmd / executor method the patched call sites and the backend use exists."""
+    backend, bsrc = _methods("RtAmdBackend.java")
+    rt, _ = _methods("RtAmd.java")
+    ex, _ = _methods("RtAmdRaytraceExecutor.java")
+    used = set()
+    for fl in _patch_files().values():
+        for line in fl["+"]:
+            used |= {("B", m) for m in re.findall(r"RtAmdBackend\.(\w+)\(", line)}
+            used |= {("E", m) for m in re.findall(r"raytraceExecutor\.(\w+)\(", line)}
+    for kind, m in sorted(used):
+        assert m in (backend if kind == "B" else ex), (kind, m)
+    for m in set(re.findall(r"(?:get\(\)|\br)\.(\w+)\(", bsrc)):
+        assert m in rt, m
+
+
+def test_binding_allocates_per_call():
+    """RtAmd keeps no long-lived arena: every call's native arguments come from a confined arena
+    closed when the call returns (the context arena grew by 33 MB per readImage)."""
+    src = open(os.path.join(JAVA, "RtAmd.java")).read()
+    assert "private final Arena" not in src and "arena." not in src
+    n_alloc = len(re.findall(r"\ba\.allocate", src))
+    n_scopes = len(re.findall(r"try \(Arena a = Arena\.ofConfined\(\)\)", src))
+    assert n_alloc >= 10 and n_scopes >= 10
+
+
+def test_executor_polls_dispatch_time_without_waiting():
+    """getLastDispatchTime refreshes on every raytrace() from the previous render's device time
+    when it is ready (rt_render_done), as the reference polls its finished timer queries."""
+    src = open(os.path.join(JAVA, "RtAmdRaytraceExecutor.java")).read()
+    body = src[src.index("public void raytrace(int n)"):]
+    body = body[:body.index("\n    }\n")]
+    assert "rt.renderDoneNanos()" in body and "lastDispatchTime" in body
