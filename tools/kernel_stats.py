@@ -27,11 +27,11 @@ def main():
     ap.add_argument("--depth", type=int, default=5)
     a = ap.parse_args()
     scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
-    ctx = rtamd.RenderContext(devices=(0,))
+    ctx = rtamd.RenderContext(devices=(0,), ab=True)   # the stats kernels are in the A/B build
     ctx.upload_scene(scene)
     ctx.set_params(max_depth=a.depth, spp=4096)
     ctx.resize(a.width, a.height)
-    L = rtamd.amd()
+    L = rtamd.amd_ab()
     assert L.rt_debug_enable_stats(ctx._h, 1) == 0
     ctx.render(1, rtamd.frame_rand_factors(1, 0, a.frames))
     ctx.sync()
