@@ -670,61 +670,6 @@ __device__ __forceinline__ uint32_t link_walk_part(const NodeSrc& ns, uint32_t n
     return nx;
 }
 
-// link_walk_part for the two-level walk: a lane whose next node lies below the LDS-staged
-// levels issues its global load at the start of a round and takes that one step at the
-// end of it, while the wave's other lanes run three LDS steps meanwhile -- so the wave
-// pays the global latency once per round, overlapped with LDS work, instead of on every
-// step in which some lane is deep.  Each lane's node sequence is unchanged.
-template <bool EXACT, bool STATS>
-__device__ __forceinline__ uint32_t link_walk_part_tl(const NodeSrc& ns, uint32_t nx, v3 o, v3 inv, float tmin,
-                                                      float tmax, int need, unsigned long long* st) {
-    for (;;) {
-        const bool deep = (int)nx >= 0 && nx >= ns.lim;
-        float4 g0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), g1 = g0;
-        if (deep) {
-            const float4* g = reinterpret_cast<const float4*>(ns.gnodes + nx);
-            g0 = ldg(g);
-            g1 = ldg(g + 1);
-        }
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            if ((int)nx >= 0 && nx < ns.lim) {
-                if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-                float4 n0, n1;
-                load_node<STATS, false>(ns, nx, n0, n1);
-                bool hit;
-                if (!EXACT) {
-                    hit = aabb_pk(n0, n1, o, inv, tmin, tmax);
-                } else {
-                    float lo = tmin, hi = tmax;
-                    slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-                    slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-                    slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-                    hit = !(hi <= lo);
-                }
-                nx = __float_as_uint(hit ? n1.z : n1.w);
-            }
-        }
-        if (deep) {   // nx is still the deep node: the lane took no LDS step this round
-            if (STATS) st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-            bool hit;
-            if (!EXACT) {
-                hit = aabb_pk(g0, g1, o, inv, tmin, tmax);
-            } else {
-                float lo = tmin, hi = tmax;
-                slab(g0.x, g0.y, o.x, inv.x, lo, hi);
-                slab(g0.z, g0.w, o.y, inv.y, lo, hi);
-                slab(g1.x, g1.y, o.z, inv.z, lo, hi);
-                hit = !(hi <= lo);
-            }
-            nx = __float_as_uint(hit ? g1.z : g1.w);
-        }
-        const unsigned long long walking = __ballot((int)nx >= 0);
-        if (walking == 0 || __popcll(__ballot(1) & ~walking) >= need) break;
-    }
-    return nx;
-}
-
 // compute.glsl:226-266 over the threaded BVH.  Each lane's node sequence is the
 // reference's; only the interleaving of a wave's lanes differs: lanes advance
 // through inner/missed nodes until each holds a hit leaf (or is done), then the
@@ -1947,12 +1892,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             if (status == RT_SM_TRACE) {
                 if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
                 unsigned long long t0 = STATS ? clock64() : 0;
-                if constexpr (TL) {
-                    const int act = __popcll(__ballot(1));
-                    const int needw = P.walk_frac >= 64 ? act : (act * P.walk_frac + 63) >> 6;
-                    nx = wave_exact ? link_walk_part_tl<true, STATS>(ns, nx, S.o, inv, 0.001f, tmax, needw, st)
-                                    : link_walk_part_tl<false, STATS>(ns, nx, S.o, inv, 0.001f, tmax, needw, st);
-                } else if (P.walk_frac >= 64) {
+                if (P.walk_frac >= 64) {
                     nx = wave_exact ? link_walk<true, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, st)
                                     : link_walk<false, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, st);
                 } else {
