@@ -85,6 +85,8 @@ enum {
     RT_OPTION_LDS_NODE_CAP = 13,        /* bytes of BVH nodes staged in LDS; the rest is
                                            read from global memory (0 = as many as fit)     */
     RT_OPTION_COMPACT_BOXES = 14,       /* canonical boxes from 48-byte LDS records (1)     */
+    RT_OPTION_SPINE = 15,               /* walks start past the root's right spine when its
+                                           boxes surely hold the ray's origin (1)           */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };
@@ -99,6 +101,7 @@ int rt_debug_get_option(struct rt_ctx* ctx, int option, int* value);
  *   out[3] box pre-test on (1/0)   out[4] dynamic LDS bytes
  *   out[5] BVH nodes staged in LDS out[6] box records: bit 0 compact tests, bit 1 in LDS
  *   out[7] staged chunks (1/0)     out[8] chunks per launch
+ *   out[9] spine nodes a walk may skip (0 = off)
  * n <= 16 ints are written; returns RT_ERR_STATE before the first render. */
 int rt_debug_last_launch(struct rt_ctx* ctx, int* out, int n);
 

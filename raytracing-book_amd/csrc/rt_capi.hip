@@ -168,6 +168,7 @@ struct rt_ctx {
     bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
     bool sph_lds = true;   // sphere records' first two float4 in LDS when they fit (env RT_SPH_LDS=0 disables; A/B)
     bool compact_boxes = true;   // boxes' compact records when every box has one (box_test_compact; option 0: A/B)
+    bool spine = true;           // walks start past the spine when they hit it for sure (plan_spine)
     int lds_node_cap = 0;        // bytes of BVH nodes staged in LDS, 0 = as many as fit (tests: force the two-level walk)
     int n_boxc_ok = 0;           // boxes whose compact record reproduces their faces
     unsigned long long watchdog_ticks = 120ull * 100000000ull;     // render_stream progress bound (100 MHz ticks)
@@ -400,6 +401,80 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
         out[2 * at + 1] = make_float4(d.zmin, d.zmax, f(hit), f(skip_at));
     }
     return out;
+}
+
+// The spine of the link-format walk (rt_kernel.hip spine_entry): every walk starts at the
+// root and, while it hits, goes on to the right child (compute.glsl:259-260), so its first
+// steps are the chain root, right child, its right child, ... down to the first leaf.  In
+// scenes with one huge object (scene 8's fog boundary, r 5000; scene 0's ground, r 1000)
+// the builder's sort puts it in the right-most leaf, and every box on the chain contains
+// it: for a ray starting inside all of them they are hits, tested on every walk (11 of
+// scene 8's ~41 node steps per walk).  Picks the longest prefix of the chain whose boxes'
+// intersection holds the camera and >= 3/4 of the leaf boxes' centres (where later walks
+// start), at least 3 nodes; its last node's hit successor is where such a walk starts.
+void plan_spine(const std::vector<float4>& L, int n_nodes, const rt_camera_ubo& cam, bool on,
+                rt_kernel_args& a) {
+    a.spine_len = 0;
+    a.spine_start = 0;
+    for (int k = 0; k < 3; k++) a.spine_lo[k] = a.spine_hi[k] = 0.0f;
+    if (!on || n_nodes <= 0 || L.size() < 2 * (size_t)n_nodes) return;
+    auto bits = [](float f) {
+        uint32_t u;
+        std::memcpy(&u, &f, 4);
+        return u;
+    };
+    std::vector<float> cx;   // leaf box centres, x y z
+    for (int i = 0; i < n_nodes; i++) {
+        if ((bits(L[2 * i + 1].z) & RT_LINK_LEAF) == 0) continue;
+        cx.push_back(0.5f * (L[2 * i].x + L[2 * i].y));
+        cx.push_back(0.5f * (L[2 * i].z + L[2 * i].w));
+        cx.push_back(0.5f * (L[2 * i + 1].x + L[2 * i + 1].y));
+    }
+    const size_t n_leaf = cx.size() / 3;
+    if (n_leaf == 0) return;
+    float lo[3] = {-INFINITY, -INFINITY, -INFINITY}, hi[3] = {INFINITY, INFINITY, INFINITY};
+    uint32_t at = 0;
+    for (int len = 1; len <= n_nodes; len++) {
+        const float4 b0 = L[2 * (at / 32)], b1 = L[2 * (at / 32) + 1];
+        const float blo[3] = {b0.x, b0.z, b1.x}, bhi[3] = {b0.y, b0.w, b1.y};
+        for (int k = 0; k < 3; k++) {
+            lo[k] = std::max(lo[k], blo[k]);
+            hi[k] = std::min(hi[k], bhi[k]);
+        }
+        float big = 0.0f;
+        bool finite = true;
+        for (int k = 0; k < 3; k++) {
+            finite = finite && std::isfinite(lo[k]) && std::isfinite(hi[k]);
+            big = std::max(big, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
+        }
+        if (!finite) break;
+        const float sh = std::ldexp(big, -18);
+        float slo[3], shi[3];
+        bool ok = true;
+        for (int k = 0; k < 3; k++) {
+            slo[k] = lo[k] + sh;
+            shi[k] = hi[k] - sh;
+            ok = ok && slo[k] < shi[k] && slo[k] < cam.camera_pos[k] && cam.camera_pos[k] < shi[k];
+        }
+        if (!ok) break;   // the intersection only shrinks along the chain
+        size_t in = 0;
+        for (size_t j = 0; j < n_leaf; j++)
+            in += cx[3 * j] > slo[0] && cx[3 * j] < shi[0] && cx[3 * j + 1] > slo[1] && cx[3 * j + 1] < shi[1] &&
+                  cx[3 * j + 2] > slo[2] && cx[3 * j + 2] < shi[2];
+        if (4 * in < 3 * n_leaf) break;
+        const uint32_t hit = bits(b1.z);
+        if (len >= 3) {
+            a.spine_len = len;
+            a.spine_start = hit;
+            for (int k = 0; k < 3; k++) {
+                a.spine_lo[k] = slo[k];
+                a.spine_hi[k] = shi[k];
+            }
+        }
+        if (hit & RT_LINK_LEAF) break;   // the chain's leaf: the walk leaves with it
+        if (hit / 32 >= (uint32_t)n_nodes) break;
+        at = hit;
+    }
 }
 
 // ---- exact near-first walk (variant 60; rt_kernel.hip trace_fast) -------------
@@ -1440,6 +1515,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
     a.debug_flags = c->debug_flags;
     a.n_lnode_f4 = (int)c->links.size();
+    plan_spine(c->links, c->n_dnodes, c->cam, c->spine, a);
     // LDS plan of the link-format shapes (rt_kernel.hip rt_launch_render): from address 0 the
     // nodes, then the leaf records, the Perlin table (6 x 256 R32F), the media records with
     // their sphere boundaries, the spheres' intersection halves (A, B) and the canonical
@@ -1969,6 +2045,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SPH_LDS: c->sph_lds = v != 0; break;
         case RT_OPTION_BIG_WG: c->big_wg = v != 0; break;
         case RT_OPTION_COMPACT_BOXES: c->compact_boxes = v != 0; break;
+        case RT_OPTION_SPINE: c->spine = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -1998,6 +2075,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_SPH_LDS: *v = c->sph_lds; break;
         case RT_OPTION_BIG_WG: *v = c->big_wg; break;
         case RT_OPTION_COMPACT_BOXES: *v = c->compact_boxes; break;
+        case RT_OPTION_SPINE: *v = c->spine; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

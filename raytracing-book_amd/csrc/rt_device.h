@@ -156,6 +156,13 @@ struct rt_kernel_args {
     int box_cmp_lds;             // float4 offset of the boxes' 48-byte records in LDS (RT_BOXC_F4 each), or
                                  // -1 (read from dboxc)
     int box_all_cmp;             // every box's record is compact (box_test_compact); else the full box test
+    // the spine (rt_capi.hip plan_spine): every walk starts with the root and its right children
+    // 1 .. spine_len-1; a ray whose origin lies in all their boxes, away from the faces by more than
+    // 0.00125 x its largest direction component, hits every one of them, so its walk starts at
+    // spine_start (the last one's hit successor).  spine_len 0: off.
+    int spine_len;
+    uint32_t spine_start;
+    float spine_lo[3], spine_hi[3];   // the boxes' intersection, shrunk by 2^-18 of its largest coordinate
     // bounds of the device-side waits, in ticks of the 100 MHz real-time clock (s_memrealtime)
     unsigned long long watchdog_ticks;     // render_stream: no sample stored by the wave for this long
                                            // -> fault word 2, the wave leaves (checked on its first pass
@@ -166,7 +173,7 @@ struct rt_kernel_args {
 
 // What rt_launch_render launched (rt_debug_last_launch)
 enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
-       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_N = 16 };
+       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_N = 16 };
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)

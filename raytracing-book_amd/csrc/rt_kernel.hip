@@ -1693,6 +1693,23 @@ __device__ __forceinline__ UnitGeo unit_geo(const KP& P, int u, int n_tiles, int
     g.total = (uint32_t)(g.wt * g.ht * (g.f1 - g.f0));
     return g;
 }
+// Where a new walk (tmin 0.001, tmax infinite) starts: the root, or past the spine (KP spine_*)
+// when the ray hits each of its boxes for sure.  Per axis k of such a box [lo, hi] with
+// lo + m < o_k < hi - m, m = 0.00125 max|d| (> 0 for a walked ray): the far slab distance is
+// (hi - o_k) / |d_k| >= m / |d_k| (1 - 3 ulp) > 0.001 (d_k = +-0: +inf, and no 0 * inf since
+// o_k != lo, hi), the near one is negative, so the reference's slab loop (hitting.glsl:55-76) keeps
+// ray_t = (0.001, min far) and reports a hit.  The host's 2^-18 shrink of the box covers the
+// rounding of lo + m and hi - m.  Non-finite o or d: the root.
+__device__ __forceinline__ uint32_t spine_entry(const KP& P, const v3& o, const v3& d) {
+    if (P.spine_len == 0) return 0u;
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const bool fin = ax <= __FLT_MAX__ && ay <= __FLT_MAX__ && az <= __FLT_MAX__;
+    const float m = 0.00125f * fmaxf(ax, fmaxf(ay, az));
+    const bool in = fin && o.x > P.spine_lo[0] + m && o.x < P.spine_hi[0] - m && o.y > P.spine_lo[1] + m &&
+                    o.y < P.spine_hi[1] - m && o.z > P.spine_lo[2] + m && o.z < P.spine_hi[2] - m;
+    return in ? P.spine_start : 0u;
+}
+
 template <bool STATS, int OPT, bool FD>
 __device__ __forceinline__ void render_stream(const KP& P, const float4* __restrict__ nodes, int gwave,
                                               unsigned long long* st) {
@@ -1871,7 +1888,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             h.uv_kind_idx = 0; h.uv_a = 0.0f; h.uv_b = 0.0f;
             has = false;
             tmax = RT_INFINITY;
-            nx = 0u;
+            nx = spine_entry(P, S.o, S.d);
             const bool dir_zero = (S.d.x == 0.0f) && (S.d.y == 0.0f) && (S.d.z == 0.0f);
             status = (dir_zero || P.n_nodes == 0) ? RT_SM_HIT : RT_SM_TRACE;
             if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);
@@ -2241,6 +2258,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         info[RT_LI_COMPACT] = a.box_all_cmp + 2 * (a.box_cmp_lds >= 0);
         info[RT_LI_STAGED] = a.samples != nullptr;
         info[RT_LI_CHUNKS] = a.n_chunks;
+        info[RT_LI_SPINE] = pool ? a.spine_len : 0;
     }
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.

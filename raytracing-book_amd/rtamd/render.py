@@ -78,11 +78,11 @@ def deinterleave(gathered, height, world, stripe_rows):
 # the A/B build only.
 OPTIONS = {"box_pretest": 1, "fastdiv": 2, "sph_lds": 3, "big_wg": 4, "chunk_target": 5,
            "staged_chunk_target": 6, "stage_tiles": 7, "sm_batch": 8, "sm_frac": 9, "walk_frac": 10,
-           "watchdog_ms": 11, "chunk_wait_ms": 12, "lds_node_cap": 13, "compact_boxes": 14,
+           "watchdog_ms": 11, "chunk_wait_ms": 12, "lds_node_cap": 13, "compact_boxes": 14, "spine": 15,
            "kernel_variant": 100, "debug_flags": 101}
 # rt_debug_last_launch fields
 LAUNCH_FIELDS = ("shape", "block", "fastdiv", "pretest", "lds_bytes", "lds_nodes", "box_records", "staged",
-                 "chunks")
+                 "chunks", "spine")
 SHAPES = {0: "fast-lds", 1: "fast-global", 2: "link-lds", 3: "meta-lds", 4: "meta-global", 5: "link-two-level"}
 
 

@@ -16,7 +16,12 @@ hit tests they target (hitting.glsl:90-146):
   * scenes scaled so their extent sits just inside / just past 2^20, where the
     shared-reciprocal division stops applying (rt_capi.hip fd_coord);
   * BVHs beyond the round-2 link-format cap of 2047 nodes, one in LDS (~4000
-    nodes) and one that needs the two-level walk (~9000 nodes).
+    nodes) and one that needs the two-level walk (~9000 nodes);
+  * walks that start past the root's right spine (rt_kernel.hip spine_entry): ray
+    origins just inside the spine's box, where its face is 0.0008 / 0.0019 / 0.01
+    ahead (the reference's slab test misses / hits just past tmin / hits), with
+    direction components up to 2 so that the entry's margin 0.00125 max|d| falls
+    inside the pixel grid; and near an edge of the box.
 Secondary bounces add random rays around the same geometry.
 """
 import numpy as np
@@ -165,6 +170,61 @@ def sphere_cloud(n, seed, W=64, H=48, boxes=True):
     return b.finish(W, H)
 
 
+def spine_box(scene):
+    """The intersection of the boxes on the threaded BVH's right spine (root, its right
+    child, ... to the first leaf): what rt_capi.hip plan_spine intersects."""
+    import ctypes
+    L = rtamd.amd()
+    bvh = scene.buffers[1]
+    raw = np.frombuffer(bvh.data if hasattr(bvh, "data") else bvh, np.uint8)
+    dn = np.dtype([("box", "<f4", (6,)), ("meta", "<u4"), ("prims", "<u4")])
+    n = ctypes.c_int()
+    assert L.rt_debug_threaded_bvh(raw.ctypes.data, raw.nbytes, None, 0, ctypes.byref(n)) == 0
+    out = np.zeros(n.value, dn)
+    assert L.rt_debug_threaded_bvh(raw.ctypes.data, raw.nbytes, out.ctypes.data, out.nbytes, ctypes.byref(n)) == 0
+    lo, hi = np.full(3, -np.inf, F32), np.full(3, np.inf, F32)
+    for nd in out:
+        bx = nd["box"]
+        lo = np.maximum(lo, bx[0::2])
+        hi = np.minimum(hi, bx[1::2])
+        if (int(nd["meta"]) >> 16) & 0xF:
+            break
+    return lo, hi, len(out)
+
+
+def spine(delta, corner=False, W=64, H=48):
+    """Scene 8's shape in small: a fog whose boundary sphere (r 50) is the BVH's largest
+    object, so it sits in the right-most leaf and every box on the right spine contains it,
+    around a cluster of small spheres and boxes; dense (2000), so rays leaving the camera
+    scatter within ~0.0005 and the next walks start from origins just inside the faces too.
+    The camera sits `delta` inside the
+    spine box's +x face on the x axis (corner: also delta below its +y face) and
+    looks along +x: d = (1, y, z), |y|, |z| <= 2, so the face is delta / 1 ahead."""
+    rng = np.random.default_rng(5)
+    b = SceneBuilder(seed=1)
+    white, red, light = _materials(b)
+    fog = b.sphere((0, 0, 0), 50.0, b.dielectric(1.5))
+    b.add(b.constant_medium(fog, 2000.0, b.isotropic(b.solid(0.9, 0.9, 0.9))))   # scatters within ~0.0005
+    for k in range(40):
+        c = tuple(float(v) for v in rng.uniform(-8, 8, 3).astype(F32))
+        b.add(b.sphere(c, 0.7, white if k % 2 else red))
+    for k in range(4):
+        b.add(b.box((-9 + 4 * k, -10, -9), (-7 + 4 * k, -9 + k, 9), white))
+    lq = b.add(b.quad((-5, 12, -5), (10, 0, 0), (0, 0, 10), light))
+    b.add_light(lq)
+    b.camera(look_from=(0, 0, 30), look_at=(0, 0, 0), vfov=40, background=(0.2, 0.25, 0.3))
+    s = b.finish(W, H)
+    lo, hi, _ = spine_box(s)
+    # on the x axis: the fog's sphere touches the box's face there, so the camera is delta
+    # inside the fog too and rays leaving it scatter (or not) right at the face
+    o = np.array([hi[0] - F32(delta), 0, 0], F32)
+    if corner:   # and delta below the +y face (outside the fog, in the box's edge region)
+        o[1] = hi[1] - F32(delta)
+    s.override_camera(grid_camera(tuple(float(v) for v in o), tuple(float(v) for v in o + F32([1, 2, -2])),
+                                  (0, 0, F32(1 / 16)), (0, -F32(1 / 12), 0)))
+    return s
+
+
 def cases():
     """The configurations, each with what its default launch must show."""
     big = 2 ** 20
@@ -183,4 +243,9 @@ def cases():
         Case("extent_past_2^20", extent(1.1 * big), expect={"fastdiv": 0, "pretest": 1}),
         Case("bvh_4k_lds", sphere_cloud(4000, 4), depth=3, frames=2, expect={"shape": 2, "block": 1024}),
         Case("bvh_9k_two_level", sphere_cloud(9000, 9), depth=3, frames=2, expect={"shape": 5, "block": 1024}),
+        Case("spine_face_0.0008", spine(0.0008)),
+        Case("spine_face_0.0019", spine(0.0019)),
+        Case("spine_face_0.01", spine(0.01)),
+        Case("spine_edge_0.0019", spine(0.0019, corner=True)),
+        Case("spine_jitter", spine(0.0019), spp=16, frames=4),
     ]

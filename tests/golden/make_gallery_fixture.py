@@ -53,6 +53,15 @@ def block_means(rgb, block):
         h // block, block, w // block, block, 3).mean(axis=(1, 3))
 
 
+def dx2(lin, m):
+    """Mean squared difference of horizontally adjacent pixels, both in the mask, per channel:
+    twice the per-pixel noise variance plus the (render-independent) texture gradient -- the
+    statistic tools/gallery_spp_probe.py matches to estimate the gallery's sample count."""
+    both = m[:, 1:] & m[:, :-1]
+    d = lin[:, 1:] - lin[:, :-1]
+    return np.round((d[both] ** 2).mean(0), 8).tolist()
+
+
 def main():
     out = {"source": "galleries/book3_final(scene6).png", "block": BLOCK}
     g = np.asarray(Image.open(os.path.join(GALLERY, "book3_final(scene6).png")).convert("RGB")).astype(np.float64)
@@ -84,6 +93,8 @@ def main():
     out["scene8_regions"] = {"source": "galleries/book2_final(scene8).png", "width": w, "height": h,
                              "regions": {k: {"n_pixels": int(m.sum()), "lin_mean": np.round(lin[m].mean(0), 6).tolist(),
                                              "byte_mean": np.round(g8[m].mean(0), 3).tolist(),
+                                             "lin_dx2": dx2(lin, m),
+                                             "frac_255": np.round((g8[m] == 255).mean(0), 6).tolist(),
                                              "all_255": bool((g8[m] == 255).all())}
                                          for k, m in regs.items()}}
     blocks = gr.block_grid(regs["earth"], EARTH_BLOCK)

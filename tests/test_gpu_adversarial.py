@@ -10,7 +10,10 @@ The shortcuts and what each case aims at:
   * the compact box records (box_test_compact): canonical boxes at exact edges,
     grazing and t = tmin; rotated boxes take the full records;
   * the link-format walk beyond 2047 nodes, in LDS (~4000 nodes) and two-level
-    (~9800 nodes: top levels in LDS, the rest from global memory).
+    (~9800 nodes: top levels in LDS, the rest from global memory);
+  * the spine entry (walks starting past the root's right spine): origins 0.0008 to
+    0.01 inside the spine box's face and edge, where the entry's margin and the
+    reference's own slab result change from pixel to pixel.
 Every case renders with the default options and with each shortcut turned off
 (rt_debug.h RT_OPTION_*); all must equal the oracle.  The launch each default
 render took is asserted (rt_debug_last_launch), so a case cannot pass by
@@ -27,7 +30,7 @@ from helpers import bit_equal, mismatch_report
 pytestmark = pytest.mark.gpu
 
 CASES = adversarial.cases()
-OFF = [{}, {"box_pretest": 0}, {"fastdiv": 0}, {"compact_boxes": 0}]
+OFF = [{}, {"box_pretest": 0}, {"fastdiv": 0}, {"compact_boxes": 0}, {"spine": 0}]
 
 
 def oracle(case):
@@ -56,6 +59,28 @@ def test_adversarial_case_matches_oracle(gpu, case):
         if not opts:
             for k, v in case.expect.items():
                 assert info[k] == v, f"{case.name}: launch {k} = {info[k]}, expected {v} ({info})"
+            if case.name.startswith("spine"):
+                assert info["spine"] == 6, info   # root + 5 right children (tests/adversarial.py spine_box)
+        elif "spine" in opts:
+            assert info["spine"] == 0, info
+
+
+def test_scene8_walks_skip_its_spine(gpu):
+    """Scene 8's right spine (11 nodes, every box +-5000: the fog's boundary sphere sits in
+    the right-most leaf) is skipped by the walks that start inside it; the same bits as
+    with the entry off and as the oracle."""
+    s = rtamd.Scene(8, 64, 48, seed=1)
+    ref = pyoracle.render(pyoracle.OracleScene(s, max_depth=5, spp=4), rtamd.frame_rand_factors(1, 0, 4))
+    for opts, want in (({}, 11), ({"spine": 0}, 0)):
+        ctx = rtamd.RenderContext(options=opts)
+        ctx.upload_scene(s)
+        ctx.set_params(max_depth=5, spp=4)
+        ctx.resize(64, 48)
+        ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+        out, info = ctx.read_image(), ctx.last_launch()
+        ctx.close()
+        assert info["spine"] == want, info
+        assert bit_equal(out, ref), f"{opts}: {mismatch_report(out, ref)}"
 
 
 @pytest.mark.parametrize("cap", [4096, 32768, 65536])
