@@ -142,6 +142,21 @@ def amd_ab():
     return _amd_ab
 
 
+_amd_at = {}
+
+
+def amd_at(path):
+    """Another build of the same ABI loaded from `path` (tools/lib_ab.py: a previous
+    revision's kernel timed beside the current one in one process)."""
+    path = os.path.abspath(path)
+    if path not in _amd_at:
+        if not os.path.exists(path):
+            raise ImportError(f"{path} is missing")
+        _import_torch_first()
+        _amd_at[path] = _amd_protos(ctypes.CDLL(path))
+    return _amd_at[path]
+
+
 def scene_lib():
     """The host scene builder (no GPU needed)."""
     global _scene

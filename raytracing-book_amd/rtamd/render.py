@@ -90,10 +90,11 @@ class RenderContext:
     """An rt_ctx: device buffers, accumulation image and launch state.
 
     ``options`` (dict name -> int, see OPTIONS) are applied right after creation;
-    ``ab=True`` uses the A/B build (librtamd_ab.so) for kernel-variant options."""
+    ``ab=True`` uses the A/B build (librtamd_ab.so) for kernel-variant options; ``lib`` a
+    library at that path (tools/lib_ab.py)."""
 
-    def __init__(self, devices=(0,), rank=0, world=1, stripe_rows=16, options=None, ab=False):
-        L = _lib.amd_ab() if ab else _lib.amd()
+    def __init__(self, devices=(0,), rank=0, world=1, stripe_rows=16, options=None, ab=False, lib=None):
+        L = _lib.amd_at(lib) if lib else (_lib.amd_ab() if ab else _lib.amd())
         self._L = L
         devs = (ctypes.c_int * len(devices))(*devices)
         h = ctypes.c_void_p()

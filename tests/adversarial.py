@@ -18,10 +18,10 @@ hit tests they target (hitting.glsl:90-146):
   * BVHs beyond the round-2 link-format cap of 2047 nodes, one in LDS (~4000
     nodes) and one that needs the two-level walk (~9000 nodes);
   * walks that start past the root's right spine (rt_kernel.hip spine_entry): ray
-    origins just inside the spine's box, where its face is 0.0008 / 0.0019 / 0.01
-    ahead (the reference's slab test misses / hits just past tmin / hits), with
-    direction components up to 2 so that the entry's margin 0.00125 max|d| falls
-    inside the pixel grid; and near an edge of the box.
+    origins just inside the spine's box, where its face is 0.0008 / 0.0019 / 0.01 ahead
+    (the reference's slab test misses / hits just past tmin / hits), with direction
+    components up to 2 so that the entry's margin 0.00125 max|d| falls inside the pixel
+    grid; and near an edge of the box.
 Secondary bounces add random rays around the same geometry.
 """
 import numpy as np

@@ -65,13 +65,15 @@ def test_adversarial_case_matches_oracle(gpu, case):
             assert info["spine"] == 0, info
 
 
-def test_scene8_walks_skip_its_spine(gpu):
+@pytest.mark.parametrize("sid,spine", [(8, 11), (0, 0)])
+def test_scenes_walks_skip_their_spine(gpu, sid, spine):
     """Scene 8's right spine (11 nodes, every box +-5000: the fog's boundary sphere sits in
-    the right-most leaf) is skipped by the walks that start inside it; the same bits as
-    with the entry off and as the oracle."""
-    s = rtamd.Scene(8, 64, 48, seed=1)
+    the right-most leaf) is skipped by the walks that start inside it; scene 0 has none
+    (its camera sits on the root box's top face, and its surfaces lie outside the ground
+    sphere's box).  The same bits as with the entry off and as the oracle."""
+    s = rtamd.Scene(sid, 64, 48, seed=1)
     ref = pyoracle.render(pyoracle.OracleScene(s, max_depth=5, spp=4), rtamd.frame_rand_factors(1, 0, 4))
-    for opts, want in (({}, 11), ({"spine": 0}, 0)):
+    for opts, want in (({}, spine), ({"spine": 0}, 0)):
         ctx = rtamd.RenderContext(options=opts)
         ctx.upload_scene(s)
         ctx.set_params(max_depth=5, spp=4)
