@@ -87,6 +87,8 @@ enum {
     RT_OPTION_COMPACT_BOXES = 14,       /* canonical boxes from 48-byte LDS records (1)     */
     RT_OPTION_SPINE = 15,               /* walks start past the root's right spine when its
                                            boxes surely hold the ray's origin (1)           */
+    RT_OPTION_TL_LEAF_LDS = 16,         /* two-level walk: leaf records in LDS beside the
+                                           top levels when they take <= half of it (1)      */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

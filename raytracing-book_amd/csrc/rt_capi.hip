@@ -170,6 +170,7 @@ struct rt_ctx {
     bool compact_boxes = true;   // boxes' compact records when every box has one (box_test_compact; option 0: A/B)
     bool spine = true;           // walks start past the spine when they hit it for sure (plan_spine)
     int lds_node_cap = 0;        // bytes of BVH nodes staged in LDS, 0 = as many as fit (tests: force the two-level walk)
+    bool tl_leaf_lds = true;     // two-level walk: the leaf records in LDS beside the top levels (when they fit)
     int n_boxc_ok = 0;           // boxes whose compact record reproduces their faces
     unsigned long long watchdog_ticks = 120ull * 100000000ull;     // render_stream progress bound (100 MHz ticks)
     unsigned long long chunk_wait_ticks = 30ull * 100000000ull;    // ordered-chunk wait bound
@@ -1578,10 +1579,16 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             at = node_f4;   // the threaded nodes (32 B each) from address 0 (rt_launch_render: META_LDS)
         } else if (!fast_walk && a.n_lnode_f4 > 0) {
             if (tl) {
-                // the top levels after the small tables the shading reads (placed below)
+                // the top levels, then the leaf records (8 B per leaf, read on every leaf visit) when
+                // they take at most half of the room, then the small tables the shading reads
                 const size_t room = cap - perlin_f4 - media_f4;
-                a.lds_node_f4 = (int)(std::min(std::min(node_f4, node_cap), room) & ~(size_t)1);
+                const size_t lf_f4 = (c->tl_leaf_lds && 2 * leaf_f4 <= room) ? leaf_f4 : 0;
+                a.lds_node_f4 = (int)(std::min(std::min(node_f4, node_cap), room - lf_f4) & ~(size_t)1);
                 at = (size_t)a.lds_node_f4;
+                if (lf_f4) {
+                    a.leaf_lds = (int)at;
+                    at += lf_f4;
+                }
             } else {
                 a.lds_node_f4 = (int)node_f4;
                 a.leaf_lds = (int)node_f4;
@@ -2046,6 +2053,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_BIG_WG: c->big_wg = v != 0; break;
         case RT_OPTION_COMPACT_BOXES: c->compact_boxes = v != 0; break;
         case RT_OPTION_SPINE: c->spine = v != 0; break;
+        case RT_OPTION_TL_LEAF_LDS: c->tl_leaf_lds = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2076,6 +2084,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_BIG_WG: *v = c->big_wg; break;
         case RT_OPTION_COMPACT_BOXES: *v = c->compact_boxes; break;
         case RT_OPTION_SPINE: *v = c->spine; break;
+        case RT_OPTION_TL_LEAF_LDS: *v = c->tl_leaf_lds; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

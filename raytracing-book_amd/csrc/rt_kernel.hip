@@ -64,6 +64,11 @@ __device__ __forceinline__ float4 ldg(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ int ldg_i(const int* p) { return *(__attribute__((address_space(1))) const int*)p; }
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 ldg_u2(const uint2* p) {
+    const u2v v = *(__attribute__((address_space(1))) const u2v*)p;
+    return make_uint2(v.x, v.y);
+}
 
 // ---- diagnostic statistics (stats variants only; never in a timed build) ----
 // Wave-level: the first active lane adds into the wave's LDS counters, so a
@@ -1727,9 +1732,11 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     ns.base = reinterpret_cast<const char*>(nodes);
     ns.gnodes = reinterpret_cast<const char*>(P.lnodes);
     ns.lim = (uint32_t)P.lds_node_f4 * 16u;
-    // the leaf records: LDS after the nodes, or (two-level) global memory after the node array
-    const uint2* __restrict__ leaves = TL ? reinterpret_cast<const uint2*>(P.lnodes + 2 * P.n_nodes)
-                                          : reinterpret_cast<const uint2*>(nodes + P.leaf_lds);
+    // the leaf records: LDS after the staged nodes, or (two-level walk, when they did not fit
+    // beside its nodes) global memory after the node array
+    const bool gleaf = TL && P.leaf_lds < 0;   // wave-uniform
+    const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + (P.leaf_lds >= 0 ? P.leaf_lds : 0));
+    const uint2* __restrict__ gleaves = reinterpret_cast<const uint2*>(P.lnodes + 2 * P.n_nodes);
     const int batch = P.sm_batch;
     // wave-uniform: the units in the two slots (-1 = free) and their stored samples;
     // the pool: its unit, slot and next unclaimed sample
@@ -1925,7 +1932,9 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                 } else {
                     unsigned long long t1 = STATS ? clock64() : 0;
                     if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-                    const uint2 lf = leaves[nx & 0x7FFFFFFFu];
+                    uint2 lf;
+                    if (gleaf) lf = ldg_u2(gleaves + (nx & 0x7FFFFFFFu));
+                    else lf = leaves[nx & 0x7FFFFFFFu];
                     leaf_prims_t<STATS, FD, BOXC>(P, lf.x << 16, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf,
                                                   fx, fy, h, has, st);
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
