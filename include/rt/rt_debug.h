@@ -89,6 +89,8 @@ enum {
                                            boxes surely hold the ray's origin (1)           */
     RT_OPTION_TL_LEAF_LDS = 16,         /* two-level walk: leaf records in LDS beside the
                                            top levels when they take <= half of it (1)      */
+    RT_OPTION_PERLIN_PACKED = 17,       /* Perlin table staged as 256 float4 with packed
+                                           perm bytes when its entries allow it (1)         */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

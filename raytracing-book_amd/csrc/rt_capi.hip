@@ -74,6 +74,7 @@ struct Device {
     DevBuf nodes, spheres, quads, boxes, media, lights, tex[8];
     DevBuf dquads, dboxes;   // intersection-only face records (rt_device.h)
     DevBuf dboxc;            // compact canonical box records (RT_BOXC_F4 per box)
+    DevBuf perlin_pk;        // the Perlin table re-laid out (rt_kernel.hip perlin_noise_pk), when it qualifies
     DevBuf image;            // internal image
     DevBuf args;             // rt_kernel_args slot in device memory
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
@@ -171,6 +172,8 @@ struct rt_ctx {
     bool spine = true;           // walks start past the spine when they hit it for sure (plan_spine)
     int lds_node_cap = 0;        // bytes of BVH nodes staged in LDS, 0 = as many as fit (tests: force the two-level walk)
     bool tl_leaf_lds = true;     // two-level walk: the leaf records in LDS beside the top levels (when they fit)
+    int perlin_pk_slot = -1;     // texture slot whose Perlin table has its packed copy (Device::perlin_pk)
+    bool perlin_pk = true;       // stage the packed Perlin table (option; else the texture as uploaded)
     int n_boxc_ok = 0;           // boxes whose compact record reproduces their faces
     unsigned long long watchdog_ticks = 120ull * 100000000ull;     // render_stream progress bound (100 MHz ticks)
     unsigned long long chunk_wait_ticks = 30ull * 100000000ull;    // ordered-chunk wait bound
@@ -1358,10 +1361,40 @@ int rt_upload_texture(rt_ctx* c, int slot, int format, int w, int h, const void*
     } else if (format != RT_TEX_RGBA8 && format != RT_TEX_R32F) {
         return set_err(c, RT_ERR_INVALID_ARG, "unknown texture format");
     }
+    // A Perlin table (texture.glsl:38-77: R32F, 6 x 256, columns ranvec x y z, perm x y z) whose
+    // perm entries are whole numbers 0..255 is also kept as 256 float4 (ranvec x y z, the three
+    // perm entries packed as bytes 0 / 1 / 2 of the fourth word): the kernel's noise then reads
+    // one float4 per lattice corner and needs no float-to-int conversions or bounds checks
+    // (every index is & 255 or an xor of bytes), the same values as the reference's texelFetch +
+    // int() of the texture (rt_kernel.hip perlin_noise_pk).
+    std::vector<float4> pk;
+    if (format == RT_TEX_R32F && w == 6 && h == 256) {
+        const float* t = (const float*)texels;
+        bool ok = true;
+        pk.resize(256);
+        for (int r = 0; r < 256 && ok; r++) {
+            uint32_t packed = 0;
+            for (int k = 0; k < 3; k++) {
+                const float v = t[r * 6 + 3 + k];
+                ok = ok && v >= 0.0f && v <= 255.0f && v == std::floor(v);
+                if (ok) packed |= (uint32_t)v << (8 * k);
+            }
+            float pf;
+            std::memcpy(&pf, &packed, 4);
+            pk[r] = make_float4(t[r * 6], t[r * 6 + 1], t[r * 6 + 2], pf);
+        }
+        if (!ok) pk.clear();
+    }
     for (Device& d : c->devs) {
         int r = dev_alloc_copy(c, d, d.tex[slot], src, bytes);
         if (r) return r;
+        if (!pk.empty()) {
+            r = dev_alloc_copy(c, d, d.perlin_pk, pk.data(), pk.size() * sizeof(float4));
+            if (r) return r;
+        }
     }
+    if (!pk.empty()) c->perlin_pk_slot = slot;
+    else if (c->perlin_pk_slot == slot) c->perlin_pk_slot = -1;
     c->tex_format[slot] = format;
     c->tex_w[slot] = w;
     c->tex_h[slot] = h;
@@ -1541,8 +1574,9 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     {
         const size_t node_f4 = 2 * (size_t)c->n_dnodes;
         const size_t leaf_f4 = (size_t)a.n_lnode_f4 > node_f4 ? (size_t)a.n_lnode_f4 - node_f4 : 0;
-        const size_t perlin_f4 =
-            a.perlin_slot >= 0 ? ((size_t)c->tex_w[a.perlin_slot] * c->tex_h[a.perlin_slot] + 3) / 4 : 0;
+        a.perlin_packed = (a.perlin_slot >= 0 && a.perlin_slot == c->perlin_pk_slot && c->perlin_pk) ? 1 : 0;
+        // the Perlin table is staged in its packed form only (else its noise reads the texture)
+        const size_t perlin_f4 = a.perlin_packed ? 256 : 0;
         const size_t media_f4 = (n_med > 0 && n_med <= 64) ? 3 * (size_t)n_med : 0;
         const size_t sph_f4 = (c->sph_lds && pooled) ? 2 * (size_t)n_sph : 0;
         const size_t box_f4 = (size_t)RT_BOXC_F4 * n_box;   // every box's record (bounds; compact faces)
@@ -1623,6 +1657,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         a.dquads = (const float4*)d.dquads.ptr;
         a.dboxes = (const float4*)d.dboxes.ptr;
         a.dboxc = (const float4*)d.dboxc.ptr;
+        a.perlin_pk = a.perlin_packed ? (const float4*)d.perlin_pk.ptr : nullptr;
         a.media = (const rt_medium*)d.media.ptr;
         a.lights = (const int32_t*)d.lights.ptr;
         for (int t = 0; t < 8; t++) {
@@ -2054,6 +2089,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_COMPACT_BOXES: c->compact_boxes = v != 0; break;
         case RT_OPTION_SPINE: c->spine = v != 0; break;
         case RT_OPTION_TL_LEAF_LDS: c->tl_leaf_lds = v != 0; break;
+        case RT_OPTION_PERLIN_PACKED: c->perlin_pk = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2085,6 +2121,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_COMPACT_BOXES: *v = c->compact_boxes; break;
         case RT_OPTION_SPINE: *v = c->spine; break;
         case RT_OPTION_TL_LEAF_LDS: *v = c->tl_leaf_lds; break;
+        case RT_OPTION_PERLIN_PACKED: *v = c->perlin_pk; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

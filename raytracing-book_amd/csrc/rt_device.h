@@ -125,6 +125,8 @@ struct rt_kernel_args {
                                  // the exact test accepts can lie outside; 0: no pre-test
     int perlin_slot;             // texture slot staged in LDS for Perlin noise (R32F, 6 x 256), or -1
     int perlin_lds;              // its float4 offset in the dynamic LDS (after the nodes), or -1
+    int perlin_packed;           // 1: LDS holds the packed table perlin_pk (256 float4), not the texture
+    const float4* perlin_pk;     // the packed Perlin table (rt_capi.hip rt_upload_texture), or nullptr
     int n_media;
     int media_lds;               // float4 offset of the media records + sphere boundaries in LDS (3 float4
                                  // per medium, after the Perlin table), or -1

@@ -835,6 +835,79 @@ __device__ __forceinline__ float perlin_noise(const float* tab, int tw, int th, 
     return accum;
 }
 
+// perlin_noise on the packed table (rt_capi.hip rt_upload_texture: row r = (ranvec r, perm_x r |
+// perm_y r << 8 | perm_z r << 16), the host having checked that every perm entry is a whole
+// number 0..255): the same lattice corners, vectors and float operations in the same order; a
+// perm value is its byte instead of int(texel), and no index can leave the table (& 255, or an
+// xor of bytes), so no bounds check.  One ds_read per corner vector, one per perm entry.
+__device__ __forceinline__ float perlin_noise_pk(const float4* tab, v3 p) {
+    float u = p.x - floorf(p.x);
+    float v = p.y - floorf(p.y);
+    float w = p.z - floorf(p.z);
+    u = u * u * (3.0f - 2.0f * u);
+    v = v * v * (3.0f - 2.0f * v);
+    w = w * w * (3.0f - 2.0f * w);
+    int i = rt_f2i(floorf(p.x));
+    int j = rt_f2i(floorf(p.y));
+    int k = rt_f2i(floorf(p.z));
+    float uu = u * u * (3.0f - 2.0f * u);
+    float vv = v * v * (3.0f - 2.0f * v);
+    float ww = w * w * (3.0f - 2.0f * w);
+    const lds_f* t = (const lds_f*)tab;
+    float accum = 0.0f;
+#pragma unroll
+    for (int di = 0; di < 2; di++) {
+        const uint32_t px = __float_as_uint(t[4 * ((i + di) & 255) + 3]) & 0xFFu;
+#pragma unroll
+        for (int dj = 0; dj < 2; dj++) {
+            const uint32_t py = (__float_as_uint(t[4 * ((j + dj) & 255) + 3]) >> 8) & 0xFFu;
+#pragma unroll
+            for (int dk = 0; dk < 2; dk++) {
+                const uint32_t pz = (__float_as_uint(t[4 * ((k + dk) & 255) + 3]) >> 16) & 0xFFu;
+                const uint32_t idx = px ^ py ^ pz;
+                const f4v cv = ((const lds_f4*)tab)[idx];
+                v3 c = mk3(cv.x, cv.y, cv.z);
+                v3 wv = mk3(u - (float)di, v - (float)dj, w - (float)dk);
+                float fi = (float)di, fj = (float)dj, fk = (float)dk;
+                accum += (fi * uu + (1.0f - fi) * (1.0f - uu)) * (fj * vv + (1.0f - fj) * (1.0f - vv)) *
+                         (fk * ww + (1.0f - fk) * (1.0f - ww)) * g_dot(c, wv);
+            }
+        }
+    }
+    return accum;
+}
+
+// noise_turb's seven octaves (texture.glsl:79-90) over the packed LDS table at float4 offset
+// `at` (inline, or as the out-of-line perlin_turb_lds) / over the texture in global memory
+// (out of line).  A call keeps the noise's registers off the walk and shading code around
+// it; which form a kernel uses is measured (texture_color).
+__device__ __forceinline__ float perlin_turb_lds_in(int at, float px, float py, float pz) {
+    const float4* tab = rt_dyn_lds + at;
+    float accum = 0.0f, weight = 1.0f;
+    v3 q = mk3(px, py, pz);
+#pragma unroll 1
+    for (int o = 0; o < 7; o++) {
+        accum += weight * perlin_noise_pk(tab, q);
+        weight *= 0.5f;
+        q = scale3(q, 2.0f);
+    }
+    return accum;
+}
+__device__ __noinline__ float perlin_turb_lds(int at, float px, float py, float pz) {
+    return perlin_turb_lds_in(at, px, py, pz);
+}
+__device__ __noinline__ float perlin_turb_global(const float* tab, int tw, int th, float px, float py, float pz) {
+    float accum = 0.0f, weight = 1.0f;
+    v3 q = mk3(px, py, pz);
+#pragma unroll 1
+    for (int o = 0; o < 7; o++) {
+        accum += weight * perlin_noise<false>(tab, tw, th, q);
+        weight *= 0.5f;
+        q = scale3(q, 2.0f);
+    }
+    return accum;
+}
+
 // texture.glsl:96-110
 __device__ __forceinline__ v2 sphere_uv(v3 p) {
     p = g_normalize(p);
@@ -858,6 +931,7 @@ __device__ __forceinline__ v2 resolve_uv(const KP& P, const UvSrc& s, float time
 }
 
 // texture.glsl:112-132
+template <bool PK_INLINE = false>
 __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvSrc& uvs, float time) {
     int detail_i = id & 0xFFF;
     int index = (id >> 12) & 0xFFFF;
@@ -882,21 +956,20 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         if (P.debug_flags & 1) return mk3s(0.5f);   // ablation only (A/B build, RT_DEBUG_FLAGS), never exact
 #endif
         float scale = ((float)detail_i / 4095.0f) * 100.0f;
-        float accum = 0.0f, weight = 1.0f;
         const bool lds = P.perlin_lds >= 0 && (index & 7) == P.perlin_slot;
-        const float* tab = lds ? reinterpret_cast<const float*>(rt_dyn_lds + P.perlin_lds)
-                               : reinterpret_cast<const float*>(T.is_float ? T.data : nullptr);
-        v3 q = p;
-#pragma unroll 1
-        for (int o = 0; o < 7; o++) {
-            accum += weight * (lds ? perlin_noise<true>(tab, T.w, T.h, q) : perlin_noise<false>(tab, T.w, T.h, q));
-            weight *= 0.5f;
-            q = scale3(q, 2.0f);
-        }
+        // PK_INLINE (the compact-box kernels, scene 8): the packed noise inline, -0.8% against the call;
+        // the other kernels call it (inline it cost them 6 more spilled VGPRs, scene 6 +1.1%)
+        const float accum = lds ? (PK_INLINE ? perlin_turb_lds_in(P.perlin_lds, p.x, p.y, p.z)
+                                             : perlin_turb_lds(P.perlin_lds, p.x, p.y, p.z))
+                                : perlin_turb_global(reinterpret_cast<const float*>(T.is_float ? T.data : nullptr),
+                                                     T.w, T.h, p.x, p.y, p.z);
         float s = 1.0f + g_sin(scale * p.z + 10.0f * fabsf(accum));
         return mk3s(0.5f * s);
     }
     if (type == RT_TEXTYPE_IMAGE) {     // texture2D: GL_LINEAR, CLAMP_TO_EDGE
+#ifdef RT_AB_KNOBS
+        if (P.debug_flags & 2) return mk3s(0.5f);   // ablation only (A/B build, RT_DEBUG_FLAGS), never exact
+#endif
         if (!T.data || T.w <= 0 || T.h <= 0) return mk3s(0.0f);
         v2 uv = resolve_uv(P, uvs, time);
         float x = uv.x * (float)T.w - 0.5f;
@@ -1289,6 +1362,7 @@ struct Path {
 
 // The shading half of ray_color's loop body (compute.glsl:310-339) for a hit.
 // Returns true when the path ended, with its color in `result`.
+template <bool PK_INLINE = false>
 __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float px, float py, v3& result) {
     v3 d = S.d;
     // hit_record of the closest hit: p = ray.o + ray.dir*t (hitting.glsl:39,104,188)
@@ -1375,7 +1449,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     }
     S.o = p;
     if (skip_pdf) {
-        S.acc = mul3(S.acc, texture_color(P, p, tex_id, S.uvs, S.time));
+        S.acc = mul3(S.acc, texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time));
         S.d = d;
         return false;
     }
@@ -1399,7 +1473,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     if (mid == RT_MAT_LAMBERTIAN) spdf = g_max(0.0f, g_dot(normal, g_normalize(d)) / RT_PI);
     else if (mid == RT_MAT_ISOTROPIC) spdf = 1.0f / (4.0f * RT_PI);
     else spdf = 0.0f;
-    v3 att = texture_color(P, p, tex_id, S.uvs, S.time);
+    v3 att = texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time);
     S.acc = mul3(S.acc, divs3(scale3(att, spdf), pdf));
     S.d = d;
     return false;
@@ -1407,6 +1481,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 
 // The rest of ray_color's loop body after the walk (compute.glsl:308-340): the
 // uv the walk left (compute.glsl:62), the background on a miss, else shade().
+template <bool PK_INLINE = false>
 __device__ __forceinline__ bool after_trace(const KP& P, Path& S, const Hit& h, bool hit, float px, float py,
                                             v3& result) {
     if (h.uv_kind_idx != 0) {
@@ -1421,7 +1496,7 @@ __device__ __forceinline__ bool after_trace(const KP& P, Path& S, const Hit& h, 
         result = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
         return true;
     }
-    return shade(P, S, h, px, py, result);
+    return shade<PK_INLINE>(P, S, h, px, py, result);
 }
 
 // One iteration of ray_color's loop (compute.glsl:304-340).
@@ -1949,7 +2024,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
             v3 cur3;
             h.t = tmax;   // the accepted hit's t (unused on a miss)
-            bool done = after_trace(P, S, h, has, fx, fy, cur3);
+            bool done = after_trace<BOXC>(P, S, h, has, fx, fy, cur3);
             if (!done && S.depth >= P.max_depth) {   // the loop is exhausted: final_color stays vec3(0)
                 cur3 = mk3s(0.0f);
                 done = true;
@@ -2030,12 +2105,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         if (LINK && P.leaf_lds >= 0)
             for (int k = tid; k < P.n_lnode_f4 - 2 * P.n_nodes; k += BLOCK)
                 s_nodes[P.leaf_lds + k] = g[2 * P.n_nodes + k];
-        if (P.perlin_lds >= 0) {   // the Perlin table after the nodes (host-sized launch)
-            const rt_dtex& T = P.tex[P.perlin_slot];
-            const float* src = reinterpret_cast<const float*>(T.data);
-            float* dst = reinterpret_cast<float*>(s_nodes + P.perlin_lds);
-            for (int k = tid; k < T.w * T.h; k += BLOCK) dst[k] = src[k];
-        }
+        if (P.perlin_lds >= 0)   // the packed Perlin table after the nodes (host-sized launch)
+            for (int k = tid; k < 256; k += BLOCK) s_nodes[P.perlin_lds + k] = ldg(P.perlin_pk + k);
         if (P.media_lds >= 0) {   // per medium: (boundary idx, type, -1/density, phase), sphere A, B
             for (int k = tid; k < 3 * P.n_media; k += BLOCK) {
                 const rt_medium& m = P.media[k / 3];

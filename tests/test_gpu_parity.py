@@ -36,6 +36,18 @@ def test_kernel_matches_oracle(gpu, scene_id, w, h, frames, depth):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
+@pytest.mark.parametrize("scene_id", [3, 5, 8])
+@pytest.mark.parametrize("packed", [1, 0])
+def test_perlin_table_forms_match_oracle(gpu, scene_id, packed):
+    """The Perlin noise (texture.glsl:38-94) from the packed LDS table (256 float4, perm entries
+    as bytes: rt_kernel.hip perlin_noise_pk) and from the texture as uploaded (global memory),
+    both bit for bit against the oracle; scenes 3, 5 and 8 carry Perlin textures."""
+    s = rtamd.Scene(scene_id, 40, 30, seed=1)
+    ref = oracle_image(s, 4, max_depth=5)
+    out = gpu_image(s, 4, max_depth=5, options={"perlin_packed": packed})
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
 def test_chunked_frames_equal_single_launch(gpu):
     """n frames in one rt_render == the same frames over several rt_render calls."""
     s = rtamd.Scene(8, 40, 24, seed=3)
