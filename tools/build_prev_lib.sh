@@ -8,7 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/raytracing-book_amd
 TMP=$(mktemp -d)
 git -C "$ROOT" show "$REV:raytracing-book_amd/csrc/rt_kernel.hip" > "$TMP/rt_kernel.hip"
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-variable -Wno-unused-function"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -Wno-unused-variable -Wno-unused-function"
 INC="-I$ROOT/include -I$PKG/csrc -I$PKG/host"
 /opt/rocm/bin/hipcc $FLAGS $INC -c -o "$TMP/k.o" "$TMP/rt_kernel.hip"
 mkdir -p "$PKG/lib/prev"

@@ -11,7 +11,7 @@ PKG = ROOT + "/raytracing-book_amd"
 
 
 def main():
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC",
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC",
            "-I" + ROOT + "/include", "-I" + PKG + "/csrc", "--cuda-device-only", "-c", "-o", "/tmp/rt_kernel_dev.o",
            PKG + "/csrc/rt_kernel.hip", "-Rpass-analysis=kernel-resource-usage"]
     if "--ab" in sys.argv:
