@@ -853,6 +853,10 @@ __device__ __forceinline__ float perlin_noise_pk(const float4* tab, v3 p) {
     float uu = u * u * (3.0f - 2.0f * u);
     float vv = v * v * (3.0f - 2.0f * v);
     float ww = w * w * (3.0f - 2.0f * w);
+    // the reference's corner weight fi * uu + (1 - fi) * (1 - uu) (texture.glsl:30-33) for fi = 0
+    // and 1: uu is a fade of a value in [0, 1], so finite and >= +0 (or NaN, which both forms
+    // propagate), hence 0 * uu = +0, 1 * x = x and x + (+0) = x: the weights are exactly
+    // 1 - uu and uu (likewise vv, ww)
     const lds_f* t = (const lds_f*)tab;
     float accum = 0.0f;
 #pragma unroll
@@ -868,9 +872,7 @@ __device__ __forceinline__ float perlin_noise_pk(const float4* tab, v3 p) {
                 const f4v cv = ((const lds_f4*)tab)[idx];
                 v3 c = mk3(cv.x, cv.y, cv.z);
                 v3 wv = mk3(u - (float)di, v - (float)dj, w - (float)dk);
-                float fi = (float)di, fj = (float)dj, fk = (float)dk;
-                accum += (fi * uu + (1.0f - fi) * (1.0f - uu)) * (fj * vv + (1.0f - fj) * (1.0f - vv)) *
-                         (fk * ww + (1.0f - fk) * (1.0f - ww)) * g_dot(c, wv);
+                accum += (di ? uu : 1.0f - uu) * (dj ? vv : 1.0f - vv) * (dk ? ww : 1.0f - ww) * g_dot(c, wv);
             }
         }
     }
