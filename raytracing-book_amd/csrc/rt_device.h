@@ -16,7 +16,9 @@
 //   textures : RGB8 expanded to RGBA8 (4 B/texel, aligned), RGBA8, R32F
 //   image    : float4 [padded_local_rows][W], stripe-compacted rows
 //   tile_done: uint32 [tiles] chunks published per 8x8 tile (ordered-chunk launches)
-//   samples  : float4 [frames][local_rows*W] per-frame colours (staged-chunk launches)
+//   samples  : float4 [frames][local_rows*W] per-frame colours (staged-chunk launches; sparse: only
+//              the colours that are not exactly zero are written)
+//   sflags   : uint8 [frames][local_rows*W] sparse staging: 1 where the colour was written
 //   wbuf     : float4 [resident waves][2][chunk_frames][64] per-wave sample colours of the
 //              units in flight (pooled units, ordered / one-chunk launches)
 #pragma once
@@ -108,6 +110,8 @@ struct rt_kernel_args {
     int n_chunks, chunk_frames;
     unsigned* tile_done;         // ordered chunks: per tile, the chunks published so far (zeroed per launch)
     float4* samples;             // staged chunks: per-frame colours [n_frames][n_pixels]; nullptr = ordered / one chunk
+    uint8_t* sflags;             // sparse staging (render_stream): per sample [n_frames][n_pixels] 1 when its colour
+                                 // is not (+0, +0, +0) and was stored in `samples`, else 0; nullptr = dense
     size_t n_pixels;             // local_rows * width
     unsigned* fault;             // set when an ordered-chunk wait times out (rt_sync reports it)
     float4* wbuf;                // pooled units, ordered / one chunk: per resident wave 2 x 64 x chunk_frames colours
@@ -175,7 +179,7 @@ struct rt_kernel_args {
 
 // What rt_launch_render launched (rt_debug_last_launch)
 enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
-       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_N = 16 };
+       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_N = 16 };
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)

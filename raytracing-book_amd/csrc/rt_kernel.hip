@@ -1954,8 +1954,12 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     if (STATS) st_add(st, ST_START_CYC, clock64() - t0);
                     if (P.max_depth <= 0) {   // the loop never runs: final_color vec3(0)
                         const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                        if (staged) P.samples[dst] = z4;
-                        else wbase[(size_t)up * slot_f4 + dst] = z4;
+                        if (staged) {
+                            if (P.sflags) P.sflags[dst] = 0;   // sparse: a zero colour is its clear flag
+                            else P.samples[dst] = z4;
+                        } else {
+                            wbase[(size_t)up * slot_f4 + dst] = z4;
+                        }
                         fin = true;
                     } else {
                         status = RT_SM_BEGIN;
@@ -2033,8 +2037,20 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             }
             if (done) {
                 const float4 c4 = make_float4(cur3.x, cur3.y, cur3.z, 0.0f);
-                if (staged) P.samples[dst] = c4;
-                else wbase[(size_t)up * slot_f4 + dst] = c4;
+                if (staged) {
+                    // sparse staging (P.sflags): every sample writes one flag byte, and only a colour
+                    // that is not exactly (+0, +0, +0) is stored; fold_kernel reads a clear flag as
+                    // that zero colour -- the same values, so the same running mean
+                    if (P.sflags) {
+                        const bool nz = (__float_as_uint(cur3.x) | __float_as_uint(cur3.y) | __float_as_uint(cur3.z)) != 0u;
+                        P.sflags[dst] = nz ? 1 : 0;
+                        if (nz) P.samples[dst] = c4;
+                    } else {
+                        P.samples[dst] = c4;
+                    }
+                } else {
+                    wbase[(size_t)up * slot_f4 + dst] = c4;
+                }
                 fin = true;
                 status = RT_SM_FRESH;
             } else {
@@ -2209,14 +2225,27 @@ __global__ void __launch_bounds__(256) fold_kernel(const KP* __restrict__ Pp) {
     float4* px = reinterpret_cast<float4*>(P.image) + pix;
     float4 prev = *px;
     const float4* s = P.samples + pix;
-    for (int f = 0; f < P.n_frames; f++) {
-        const float4 cur = s[(size_t)f * P.n_pixels];
-        const int fc = P.first_frame + f;
-        const float n1 = (float)(fc - 1), n = (float)fc;
-        prev.x = (prev.x * n1 + cur.x) / n;
-        prev.y = (prev.y * n1 + cur.y) / n;
-        prev.z = (prev.z * n1 + cur.z) / n;
-        prev.w = 1.0f;
+    if (P.sflags) {   // sparse staging: a clear flag is the colour (+0, +0, +0), never stored
+        const uint8_t* fl = P.sflags + pix;
+        for (int f = 0; f < P.n_frames; f++) {
+            const float4 cur = fl[(size_t)f * P.n_pixels] ? s[(size_t)f * P.n_pixels] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const int fc = P.first_frame + f;
+            const float n1 = (float)(fc - 1), n = (float)fc;
+            prev.x = (prev.x * n1 + cur.x) / n;
+            prev.y = (prev.y * n1 + cur.y) / n;
+            prev.z = (prev.z * n1 + cur.z) / n;
+            prev.w = 1.0f;
+        }
+    } else {
+        for (int f = 0; f < P.n_frames; f++) {
+            const float4 cur = s[(size_t)f * P.n_pixels];
+            const int fc = P.first_frame + f;
+            const float n1 = (float)(fc - 1), n = (float)fc;
+            prev.x = (prev.x * n1 + cur.x) / n;
+            prev.y = (prev.y * n1 + cur.y) / n;
+            prev.z = (prev.z * n1 + cur.z) / n;
+            prev.w = 1.0f;
+        }
     }
     *px = prev;
 }
@@ -2341,6 +2370,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         info[RT_LI_STAGED] = a.samples != nullptr;
         info[RT_LI_CHUNKS] = a.n_chunks;
         info[RT_LI_SPINE] = pool ? a.spine_len : 0;
+        info[RT_LI_SPARSE] = a.samples && a.sflags ? 1 : 0;
     }
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.
@@ -2354,6 +2384,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
     if (a.n_chunks > 1 && !a.samples &&
         hipMemsetAsync(a.tile_done, 0, sizeof(unsigned) * (size_t)n_tiles, st) != hipSuccess)
         return -1;
+
     constexpr int SM = RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM;
     // the instantiations: <LINK, MINW, STATS, LDSN, BLOCK, FAST, OPT>
 #ifdef RT_AB_KNOBS

@@ -112,6 +112,30 @@ def test_exactness_shortcuts_change_no_bit_1080p(gpu, knob, sid):
     assert bit_equal(on, off), mismatch_report(on, off)
 
 
+@pytest.mark.parametrize("world,rank", [(1, 0), (8, 3)])
+@pytest.mark.parametrize("sid", [8, 0, 6])
+def test_sparse_staging_changes_no_bit_1080p(gpu, sid, world, rank):
+    """Sparse staging: every sample writes a flag byte and only the colours that are
+    not exactly zero their 16 bytes; fold_kernel reads a clear flag back as the zero colour.
+    Against dense staging, whole 1080p images of 16 frames continuing an
+    accumulation (and one rank of 8 over 96 frames), the same bits; the default launch must
+    have taken the sparse form."""
+    scene = rtamd.Scene(sid, 1920, 1080, seed=1)
+    imgs = []
+    for opts in ({}, {"sparse_stage": 0}):
+        ctx = rtamd.RenderContext(devices=(0,), rank=rank, world=world, stripe_rows=8, options=opts)
+        ctx.upload_scene(scene)
+        ctx.set_params(max_depth=5, spp=4096)
+        ctx.resize(1920, 1080)
+        ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+        ctx.render(5, rtamd.frame_rand_factors(1, 4, 16 if world == 1 else 96))
+        info = ctx.last_launch()
+        imgs.append(ctx.read_image())
+        ctx.close()
+        assert info["staged"] == 1 and info["sparse"] == (0 if opts else 1), info
+    assert bit_equal(imgs[0], imgs[1]), mismatch_report(imgs[0], imgs[1])
+
+
 @pytest.mark.parametrize("sid", [8, 0])
 @pytest.mark.parametrize("knob", ["big_wg", "sph_lds"])
 def test_lds_record_copies_change_no_bit_1080p(gpu, knob, sid):
