@@ -92,7 +92,9 @@ enum {
     RT_OPTION_PERLIN_PACKED = 17,       /* Perlin table staged as 256 float4 with packed
                                            perm bytes when its entries allow it (1)         */
     RT_OPTION_SPARSE_STAGE = 18,        /* staged chunks write only colours that are not
-                                           exactly zero, plus per-pixel frame bits (1)      */
+                                           exactly zero, plus a flag byte per sample (1)    */
+    RT_OPTION_SPHERE_PAIRS = 19,        /* kernels testing a two-sphere leaf's spheres at
+                                           once, when most leaves are such pairs (1)        */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };
@@ -108,7 +110,8 @@ int rt_debug_get_option(struct rt_ctx* ctx, int option, int* value);
  *   out[5] BVH nodes staged in LDS out[6] box records: bit 0 compact tests, bit 1 in LDS
  *   out[7] staged chunks (1/0)     out[8] chunks per launch
  *   out[9] spine nodes a walk may skip (0 = off)
- *   out[10] sparse staging (1 = only non-zero colours stored, with frame bits)
+ *   out[10] sparse staging (1 = a flag byte per sample, only non-zero colours stored)
+ *   out[11] sphere-pair kernel (1 = a two-sphere leaf's spheres tested at once)
  * n <= 16 ints are written; returns RT_ERR_STATE before the first render. */
 int rt_debug_last_launch(struct rt_ctx* ctx, int* out, int n);
 

@@ -175,6 +175,8 @@ struct rt_ctx {
     bool tl_leaf_lds = true;     // two-level walk: the leaf records in LDS beside the top levels (when they fit)
     int perlin_pk_slot = -1;     // texture slot whose Perlin table has its packed copy (Device::perlin_pk)
     bool sparse_stage = true;    // staged chunks store only the colours that are not exactly zero (option)
+    bool sphere_pairs = true;    // the sphere-pair kernels when most leaves hold two spheres (option)
+    int pair_leaves = -1;        // per mille of the link-format leaves that hold two spheres (< 0: not counted)
     bool perlin_pk = true;       // stage the packed Perlin table (option; else the texture as uploaded)
     int n_boxc_ok = 0;           // boxes whose compact record reproduces their faces
     unsigned long long watchdog_ticks = 120ull * 100000000ull;     // render_stream progress bound (100 MHz ticks)
@@ -947,6 +949,7 @@ int validate(rt_ctx* c) {
     c->fast = build_fast(c->dnodes, ns, (const rt_quad*)QB.data(), nq, (const rt_box*)BB.data(), nb);
     c->fast.ok = c->fast.ok && c->spec_ok && !c->uv_always;
     c->links = build_links(c->dnodes);
+    c->pair_leaves = -1;
     c->fast_gen++;
     c->validated = true;
     return RT_OK;
@@ -1570,6 +1573,26 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.n_sph_lds = n_sph;
     a.n_box_lds = n_box;
     a.box_all_cmp = (c->compact_boxes && n_box > 0 && c->n_boxc_ok == n_box) ? 1 : 0;
+    // the sphere-pair kernels (rt_kernel.hip leaf_prims_t SPAIR) for a BVH whose leaves are mostly
+    // two spheres (scene 0: 485 spheres); measured slower where they are not
+    if (c->pair_leaves < 0) {
+        size_t n = 0, pairs = 0;
+        const size_t nf4 = 2 * (size_t)c->n_dnodes;
+        for (int i = 0; i < c->n_dnodes && c->links.size() > nf4; i++) {
+            uint32_t hs;
+            std::memcpy(&hs, &c->links[2 * (size_t)i + 1].z, 4);
+            if (!(hs & RT_LINK_LEAF)) continue;
+            const size_t ord = hs & 0x7FFFFFFFu;
+            if (nf4 + ord / 2 >= c->links.size()) continue;
+            uint32_t w[4];
+            std::memcpy(w, &c->links[nf4 + ord / 2], 16);
+            const uint32_t types = w[2 * (ord % 2)] & 0xFFu;
+            n++;
+            pairs += types == (uint32_t)(RT_MODEL_SPHERE | (RT_MODEL_SPHERE << 4));
+        }
+        c->pair_leaves = n ? (int)(1000 * pairs / n) : 0;
+    }
+    a.sph_pairs = (c->sphere_pairs && c->pair_leaves >= 500) ? 1 : 0;
     a.perlin_slot = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
@@ -2107,6 +2130,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_TL_LEAF_LDS: c->tl_leaf_lds = v != 0; break;
         case RT_OPTION_PERLIN_PACKED: c->perlin_pk = v != 0; break;
         case RT_OPTION_SPARSE_STAGE: c->sparse_stage = v != 0; break;
+        case RT_OPTION_SPHERE_PAIRS: c->sphere_pairs = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2140,6 +2164,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_TL_LEAF_LDS: *v = c->tl_leaf_lds; break;
         case RT_OPTION_PERLIN_PACKED: *v = c->perlin_pk; break;
         case RT_OPTION_SPARSE_STAGE: *v = c->sparse_stage; break;
+        case RT_OPTION_SPHERE_PAIRS: *v = c->sphere_pairs; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

@@ -162,6 +162,7 @@ struct rt_kernel_args {
     int box_cmp_lds;             // float4 offset of the boxes' 48-byte records in LDS (RT_BOXC_F4 each), or
                                  // -1 (read from dboxc)
     int box_all_cmp;             // every box's record is compact (box_test_compact); else the full box test
+    int sph_pairs;               // most leaves hold two spheres: the kernels that test such a leaf's two at once
     // the spine (rt_capi.hip plan_spine): every walk starts with the root and its right children
     // 1 .. spine_len-1; a ray whose origin lies in all their boxes, away from the faces by more than
     // 0.00125 x its largest direction component, hits every one of them, so its walk starts at
@@ -179,7 +180,7 @@ struct rt_kernel_args {
 
 // What rt_launch_render launched (rt_debug_last_launch)
 enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
-       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_N = 16 };
+       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_N = 16 };
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)

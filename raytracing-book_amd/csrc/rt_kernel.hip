@@ -44,6 +44,7 @@ typedef rt_kernel_args KP;
 #define RT_OPT_STREAM 8 // with RT_OPT_SM: the wave streams over units (render_stream) instead of one at a time
 #define RT_OPT_TL 16    // with RT_OPT_STREAM: two-level walk (top levels in LDS, the rest of the nodes global)
 #define RT_OPT_BOXC 32  // with RT_OPT_STREAM: every box has a compact record (box_test_compact), no full box test
+#define RT_OPT_SPAIR 64 // with RT_OPT_STREAM: leaves of two spheres tested at once (leaf_prims_t; most leaves are)
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -186,6 +187,23 @@ __device__ __forceinline__ bool sphere_t_ab(float4 A, float4 B, float time, v3 o
         if (!(tmin < root && root < tmax)) return false;
     }
     t = root;
+    return true;
+}
+// sphere_t_ab's quadratic with both roots, (-b - sq) / a and (-b + sq) / a, whatever ray_t is
+// (false when the discriminant is negative); the division form as sphere_t_ab chooses it.
+__device__ __forceinline__ bool sphere_roots(float4 A, float4 B, float time, v3 o, v3 d, float a, float& lo, float& hi,
+                                             bool fd) {
+    v3 center = add3(f3(A), scale3(f3(B), time));
+    v3 oc = sub3(o, center);
+    float half_b = g_dot(oc, d);
+    float c = g_dot(oc, oc) - B.w * B.w;
+    float disc = half_b * half_b - a * c;
+    if (disc < 0.0f) return false;
+    float sq = sqrtf(disc);
+    fd = fd && __ballot(!(a >= 0x1p-60f)) == 0;
+    const float ra = fd ? rcp_nr(a) : 0.0f;
+    lo = fd ? div_nr(-half_b - sq, a, ra) : (-half_b - sq) / a;
+    hi = fd ? div_nr(-half_b + sq, a, ra) : (-half_b + sq) / a;
     return true;
 }
 __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
@@ -503,11 +521,48 @@ __device__ __forceinline__ bool aabb_pk(float4 n0, float4 n1, v3 o, v3 inv, floa
 
 // The two prims of a leaf (compute.glsl:247-256), left then right.
 // FD: the shared-reciprocal divisions (rcp_nr / div_nr; FD kernels only).
-template <bool STATS, bool FD, bool BOXC = false>
+template <bool STATS, bool FD, bool BOXC = false, bool SPAIR = false>
 __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, v3 inv, float a,
                                              float time, float tmin, float& tmax, float& rf, float px, float py, Hit& h,
                                              bool& has, unsigned long long* st) {
     constexpr bool fd = FD;
+    // A leaf of two spheres (the sphere cluster's leaves; a singleton sphere leaf tests its sphere
+    // twice, Q7): both quadratics and all four roots at once, then the reference's selection of
+    // each sphere in turn (hitting.glsl:28-34) under the ray_t.max the first one leaves.  A root
+    // does not depend on ray_t, so this is sphere_t_ab twice in order: the same values, the same
+    // hits, the two records' loads and dependent chains overlapped.
+    // Only in the SPAIR kernels (scenes whose leaves are mostly sphere pairs, rt_capi.hip): where
+    // most lanes hold other leaves, the extra block costs more than it saves (scene 8 +1%, and
+    // the code alone scene 6 +1.3%); scene 0 -6.1%.
+    if (SPAIR && !STATS && P.sph_lds >= 0 && ((meta >> 16) & 0xFFu) == (RT_MODEL_SPHERE | (RT_MODEL_SPHERE << 4))) {
+        const int i0 = (int)(prims & 0xFFFFu), i1 = (int)(prims >> 16);
+        const float4* r0 = rt_dyn_lds + P.sph_lds + 2 * i0;
+        const float4* r1 = rt_dyn_lds + P.sph_lds + 2 * i1;
+        const float4 A0 = r0[0], B0 = r0[1], A1 = r1[0], B1 = r1[1];
+        float lo0, hi0, lo1, hi1;
+        const bool ok0 = sphere_roots(A0, B0, time, o, d, a, lo0, hi0, fd);
+        const bool ok1 = sphere_roots(A1, B1, time, o, d, a, lo1, hi1, fd);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const bool ok = k ? ok1 : ok0;
+            const int ix = k ? i1 : i0;
+            float root = k ? lo1 : lo0;
+            bool hit = ok && tmin < root && root < tmax;
+            if (ok && !hit) {
+                root = k ? hi1 : hi0;
+                hit = tmin < root && root < tmax;
+            }
+            if (hit) {
+                h.uv_kind_idx = (1 << 16) | ix;
+                h.uv_a = root;
+                has = true;
+                tmax = root;
+                h.t = root;
+                h.tif = RT_MODEL_SPHERE | (ix << 16);
+            }
+        }
+        return;
+    }
     // finite origin and direction: the canonical box planes equal the reference's dot products
     const bool fin = fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY &&
                      fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY;
@@ -2016,7 +2071,8 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     uint2 lf;
                     if (gleaf) lf = ldg_u2(gleaves + (nx & 0x7FFFFFFFu));
                     else lf = leaves[nx & 0x7FFFFFFFu];
-                    leaf_prims_t<STATS, FD, BOXC>(P, lf.x << 16, lf.y, S.o, S.d, inv, a, S.time, 0.001f, tmax, S.rf,
+                    leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0>(P, lf.x << 16, lf.y, S.o, S.d, inv, a,
+                                                                             S.time, 0.001f, tmax, S.rf,
                                                   fx, fy, h, has, st);
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
                     nx = lf.x >> 8;   // the leaf's skip node
@@ -2371,6 +2427,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         info[RT_LI_CHUNKS] = a.n_chunks;
         info[RT_LI_SPINE] = pool ? a.spine_len : 0;
         info[RT_LI_SPARSE] = a.samples && a.sflags ? 1 : 0;
+        info[RT_LI_SPAIR] = (pool && shape == LINK_LDS && a.sph_pairs && !a.box_all_cmp && a.sph_lds >= 0) ? 1 : 0;
     }
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.
@@ -2402,6 +2459,12 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
                                 : RT_KERNEL(true, true, BLOCK, false, (OPT) | RT_OPT_FD))                     \
                : (a.box_all_cmp ? RT_KERNEL(true, true, BLOCK, false, (OPT) | RT_OPT_BOXC)                    \
                                 : RT_KERNEL(true, true, BLOCK, false, (OPT))))
+    // ... and, for a scene whose leaves are mostly sphere pairs (a.sph_pairs), without compact boxes
+#define RT_LINK4S(BLOCK, OPT)                                                                                 \
+    ((a.sph_pairs && !a.box_all_cmp)                                                                         \
+         ? (a.fastdiv ? RT_KERNEL(true, true, BLOCK, false, (OPT) | RT_OPT_FD | RT_OPT_SPAIR)                \
+                      : RT_KERNEL(true, true, BLOCK, false, (OPT) | RT_OPT_SPAIR))                          \
+         : RT_LINK4(BLOCK, OPT))
     switch (shape) {
         case LINK_LDS:
             if (!pool) {
@@ -2409,9 +2472,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
                 rc = RT_KERNEL(true, true, 512, false, 0);
 #endif
             } else if (a.block == 1024) {
-                rc = RT_LINK4(1024, SM);
+                rc = RT_LINK4S(1024, SM);
             } else {
-                rc = RT_LINK4(512, SM);
+                rc = RT_LINK4S(512, SM);
             }
             break;
         case LINK_TL: rc = RT_LINK4(1024, SM | RT_OPT_TL); break;
@@ -2425,6 +2488,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
     }
 #undef RT_KERNEL
 #undef RT_LINK4
+#undef RT_LINK4S
     if (rc) return rc;
     if (a.samples) {   // staged chunks: the running mean over the launch's frames
         const unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);

@@ -48,6 +48,25 @@ def test_perlin_table_forms_match_oracle(gpu, scene_id, packed):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
+@pytest.mark.parametrize("scene_id,pairs", [(0, 1), (1, 1), (9, 1), (8, 0), (6, 0)])
+def test_sphere_pair_kernel_matches_oracle(gpu, scene_id, pairs):
+    """Scenes whose leaves are mostly two spheres take the kernels that test both at once
+    (rt_kernel.hip leaf_prims_t SPAIR; scene 0's 485 spheres), the others not; with the option
+    off every scene takes the plain kernels.  Both bit for bit against the oracle."""
+    s = rtamd.Scene(scene_id, 48, 27, seed=1)
+    ref = oracle_image(s, 4, max_depth=5)
+    for opts, want in (({}, pairs), ({"sphere_pairs": 0}, 0)):
+        ctx = rtamd.RenderContext(options=opts)
+        ctx.upload_scene(s)
+        ctx.set_params(max_depth=5, spp=4)
+        ctx.resize(48, 27)
+        ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+        out, info = ctx.read_image(), ctx.last_launch()
+        ctx.close()
+        assert info["sphere_pairs"] == want, (opts, info)
+        assert bit_equal(out, ref), f"{opts}: {mismatch_report(out, ref)}"
+
+
 def test_chunked_frames_equal_single_launch(gpu):
     """n frames in one rt_render == the same frames over several rt_render calls."""
     s = rtamd.Scene(8, 40, 24, seed=3)
