@@ -381,8 +381,10 @@ __device__ __noinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3
 // Both boundary hit_sphere calls (:165, :168) see the same ray and sphere: the
 // quadratic and both roots are computed once, then each call's root selection
 // is applied to its own interval.
+// fd: the two roots share rcp_nr(a) (the sphere roots' regime, sphere_t_ab: the wave falls back
+// to '/' when a lane's a = dot(dir, dir) is below 2^-60).
 __device__ __forceinline__ bool sphere_bounds(float4 A, float4 B, v3 o, v3 d, float a, float time, float& t1,
-                                              float& t2) {
+                                              float& t2, bool fd = false) {
     {
         v3 center = add3(f3(A), scale3(f3(B), time));
         v3 oc = sub3(o, center);
@@ -391,8 +393,10 @@ __device__ __forceinline__ bool sphere_bounds(float4 A, float4 B, v3 o, v3 d, fl
         float disc = half_b * half_b - a * c;
         if (disc < 0.0f) return false;
         float sq = sqrtf(disc);
-        float r_lo = (-half_b - sq) / a;
-        float r_hi = (-half_b + sq) / a;
+        fd = fd && __ballot(!(a >= 0x1p-60f)) == 0;
+        const float ra = fd ? rcp_nr(a) : 0.0f;
+        float r_lo = fd ? div_nr(-half_b - sq, a, ra) : (-half_b - sq) / a;
+        float r_hi = fd ? div_nr(-half_b + sq, a, ra) : (-half_b + sq) / a;
         if (-RT_INFINITY < r_lo && r_lo < RT_INFINITY) t1 = r_lo;
         else if (-RT_INFINITY < r_hi && r_hi < RT_INFINITY) t1 = r_hi;
         else return false;
@@ -431,6 +435,7 @@ __device__ __forceinline__ bool medium_tail(float neg_inv_density, float t1, flo
 }
 
 // hitting.glsl:162-193 — returns the hit distance t.
+template <bool FD = false>
 __device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin,
                                             float tmax, float& rf, float px, float py, float& t) {
     float t1, t2;
@@ -444,7 +449,7 @@ __device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, fl
         m.phase_material = __float_as_int(R0.w);
         m.texture_id = 0;
         if (m.boundary_type == RT_MODEL_SPHERE) {
-            if (!sphere_bounds(r[1], r[2], o, d, a, time, t1, t2)) return false;
+            if (!sphere_bounds(r[1], r[2], o, d, a, time, t1, t2, FD)) return false;
         } else if (!medium_bounds(P, m, o, d, a, time, t1, t2)) {
             return false;
         }
@@ -630,7 +635,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
-            hit = medium_test(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
+            hit = medium_test<FD>(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
             if (STATS) st_add(st, ST_MED_CYC, clock64() - c0);
         }
         if (hit) {
@@ -2282,8 +2287,29 @@ __global__ void __launch_bounds__(256) fold_kernel(const KP* __restrict__ Pp) {
     float4 prev = *px;
     const float4* s = P.samples + pix;
     if (P.sflags) {   // sparse staging: a clear flag is the colour (+0, +0, +0), never stored
+        // eight frames at a time: their flags, then the set ones' colours, all loads issued
+        // before the eight folds (which stay in frame order)
         const uint8_t* fl = P.sflags + pix;
-        for (int f = 0; f < P.n_frames; f++) {
+        int f = 0;
+        for (; f + 8 <= P.n_frames; f += 8) {
+            uint32_t fb[8];
+            float4 cur[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) fb[k] = fl[(size_t)(f + k) * P.n_pixels];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                cur[k] = fb[k] ? s[(size_t)(f + k) * P.n_pixels] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int fc = P.first_frame + f + k;
+                const float n1 = (float)(fc - 1), n = (float)fc;
+                prev.x = (prev.x * n1 + cur[k].x) / n;
+                prev.y = (prev.y * n1 + cur[k].y) / n;
+                prev.z = (prev.z * n1 + cur[k].z) / n;
+                prev.w = 1.0f;
+            }
+        }
+        for (; f < P.n_frames; f++) {
             const float4 cur = fl[(size_t)f * P.n_pixels] ? s[(size_t)f * P.n_pixels] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             const int fc = P.first_frame + f;
             const float n1 = (float)(fc - 1), n = (float)fc;
