@@ -36,6 +36,16 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
  * there is no BVH. */
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4);
 
+/* Host-only: the packed Perlin table rt_upload_texture keeps beside an R32F 6 x 256 texture
+ * whose perm columns (3..5) hold whole numbers 0..255: 256 float4 (ranvec x, y, z; the three
+ * perm entries as bytes 0, 1, 2 of the fourth word).  Returns 1 (table written to out when
+ * out != NULL), 0 when the texture does not qualify (the kernel then reads it as uploaded). */
+int rt_debug_perlin_pack(const float* texels, int w, int h, void* out, size_t out_cap);
+
+/* Host-only: per mille of a reference BVH upload's leaves that hold two spheres; rt_render
+ * takes the sphere-pair kernels at >= 500 (and when the boxes are not all canonical). */
+int rt_debug_sphere_pair_leaves(const void* bvh, size_t nbytes, int* permille);
+
 /* Host-only: rt_read_image's device de-interleave (deinterleave_kernel) with the same
  * row indexing (rt_device.h rt_gathered_row), on the host (tests compare it with
  * rt_deinterleave_rows). */

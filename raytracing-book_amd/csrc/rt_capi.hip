@@ -1348,6 +1348,49 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
     return RT_OK;
 }
 
+// The packed Perlin table (rt_kernel.hip perlin_noise_pk): 256 float4 (ranvec x y z, perm x |
+// perm y << 8 | perm z << 16) from an R32F 6 x 256 texture whose perm columns hold whole
+// numbers 0..255; false (and pk empty) for any other texture.
+bool perlin_pack(const float* t, int w, int h, std::vector<float4>& pk) {
+    pk.clear();
+    if (!t || w != 6 || h != 256) return false;
+    pk.resize(256);
+    for (int r = 0; r < 256; r++) {
+        uint32_t packed = 0;
+        for (int k = 0; k < 3; k++) {
+            const float v = t[r * 6 + 3 + k];
+            if (!(v >= 0.0f && v <= 255.0f && v == std::floor(v))) {
+                pk.clear();
+                return false;
+            }
+            packed |= (uint32_t)v << (8 * k);
+        }
+        float pf;
+        std::memcpy(&pf, &packed, 4);
+        pk[r] = make_float4(t[r * 6], t[r * 6 + 1], t[r * 6 + 2], pf);
+    }
+    return true;
+}
+
+// Per mille of the link-format leaves (build_links) that hold two spheres: the sphere-pair
+// kernels' criterion (rt_render: at least 500).
+int pair_leaves_permille(const std::vector<float4>& L, int n_nodes) {
+    size_t n = 0, pairs = 0;
+    const size_t nf4 = 2 * (size_t)n_nodes;
+    for (int i = 0; i < n_nodes && L.size() > nf4; i++) {
+        uint32_t hs;
+        std::memcpy(&hs, &L[2 * (size_t)i + 1].z, 4);
+        if (!(hs & RT_LINK_LEAF)) continue;
+        const size_t ord = hs & 0x7FFFFFFFu;
+        if (nf4 + ord / 2 >= L.size()) continue;
+        uint32_t w[4];
+        std::memcpy(w, &L[nf4 + ord / 2], 16);
+        n++;
+        pairs += (w[2 * (ord % 2)] & 0xFFu) == (uint32_t)(RT_MODEL_SPHERE | (RT_MODEL_SPHERE << 4));
+    }
+    return n ? (int)(1000 * pairs / n) : 0;
+}
+
 int rt_upload_texture(rt_ctx* c, int slot, int format, int w, int h, const void* texels) {
     if (!c) return RT_ERR_INVALID_ARG;
     if (slot < 0 || slot >= RT_MAX_TEXTURES) return set_err(c, RT_ERR_LIMIT, "texture slot must be 0..7");
@@ -1373,23 +1416,7 @@ int rt_upload_texture(rt_ctx* c, int slot, int format, int w, int h, const void*
     // (every index is & 255 or an xor of bytes), the same values as the reference's texelFetch +
     // int() of the texture (rt_kernel.hip perlin_noise_pk).
     std::vector<float4> pk;
-    if (format == RT_TEX_R32F && w == 6 && h == 256) {
-        const float* t = (const float*)texels;
-        bool ok = true;
-        pk.resize(256);
-        for (int r = 0; r < 256 && ok; r++) {
-            uint32_t packed = 0;
-            for (int k = 0; k < 3; k++) {
-                const float v = t[r * 6 + 3 + k];
-                ok = ok && v >= 0.0f && v <= 255.0f && v == std::floor(v);
-                if (ok) packed |= (uint32_t)v << (8 * k);
-            }
-            float pf;
-            std::memcpy(&pf, &packed, 4);
-            pk[r] = make_float4(t[r * 6], t[r * 6 + 1], t[r * 6 + 2], pf);
-        }
-        if (!ok) pk.clear();
-    }
+    if (format == RT_TEX_R32F && !perlin_pack((const float*)texels, w, h, pk)) pk.clear();
     for (Device& d : c->devs) {
         int r = dev_alloc_copy(c, d, d.tex[slot], src, bytes);
         if (r) return r;
@@ -1575,23 +1602,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.box_all_cmp = (c->compact_boxes && n_box > 0 && c->n_boxc_ok == n_box) ? 1 : 0;
     // the sphere-pair kernels (rt_kernel.hip leaf_prims_t SPAIR) for a BVH whose leaves are mostly
     // two spheres (scene 0: 485 spheres); measured slower where they are not
-    if (c->pair_leaves < 0) {
-        size_t n = 0, pairs = 0;
-        const size_t nf4 = 2 * (size_t)c->n_dnodes;
-        for (int i = 0; i < c->n_dnodes && c->links.size() > nf4; i++) {
-            uint32_t hs;
-            std::memcpy(&hs, &c->links[2 * (size_t)i + 1].z, 4);
-            if (!(hs & RT_LINK_LEAF)) continue;
-            const size_t ord = hs & 0x7FFFFFFFu;
-            if (nf4 + ord / 2 >= c->links.size()) continue;
-            uint32_t w[4];
-            std::memcpy(w, &c->links[nf4 + ord / 2], 16);
-            const uint32_t types = w[2 * (ord % 2)] & 0xFFu;
-            n++;
-            pairs += types == (uint32_t)(RT_MODEL_SPHERE | (RT_MODEL_SPHERE << 4));
-        }
-        c->pair_leaves = n ? (int)(1000 * pairs / n) : 0;
-    }
+    if (c->pair_leaves < 0) c->pair_leaves = pair_leaves_permille(c->links, c->n_dnodes);
     a.sph_pairs = (c->sphere_pairs && c->pair_leaves >= 500) ? 1 : 0;
     a.perlin_slot = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
@@ -2027,6 +2038,27 @@ int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_ca
         if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
         std::memcpy(out, L.data(), L.size() * sizeof(float4));
     }
+    return RT_OK;
+}
+
+int rt_debug_perlin_pack(const float* texels, int w, int h, void* out, size_t out_cap) {
+    if (!texels || w <= 0 || h <= 0) return RT_ERR_INVALID_ARG;
+    std::vector<float4> pk;
+    if (!perlin_pack(texels, w, h, pk)) return 0;
+    if (out) {
+        if (out_cap < pk.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
+        std::memcpy(out, pk.data(), pk.size() * sizeof(float4));
+    }
+    return 1;
+}
+
+int rt_debug_sphere_pair_leaves(const void* bvh, size_t nbytes, int* permille) {
+    if (!bvh || !permille || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
+    std::vector<rt_dnode> dn;
+    rt_ctx tmp;
+    int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
+    if (r) return r;
+    *permille = pair_leaves_permille(build_links(dn), (int)dn.size());
     return RT_OK;
 }
 

@@ -98,6 +98,8 @@ def _amd_protos(L):
            ctypes.POINTER(ctypes.c_uint32), sz, c_int_p, c_int_p)
     _proto(L, "rt_debug_link_nodes", i, vp, sz, vp, sz, c_int_p)
     _proto(L, "rt_debug_box_records", i, vp, sz, vp, sz, c_int_p)
+    _proto(L, "rt_debug_perlin_pack", i, c_float_p, i, i, vp, sz)
+    _proto(L, "rt_debug_sphere_pair_leaves", i, vp, sz, c_int_p)
     _proto(L, "rt_debug_deinterleave", i, c_float_p, i, i, i, i, c_float_p)
     _proto(L, "rt_debug_device_count", i)
     _proto(L, "rt_debug_enable_stats", i, vp, i)

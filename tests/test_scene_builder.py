@@ -159,3 +159,57 @@ def test_builder_errors():
     assert s.info["n_quads"] == 2 and s.info["n_bvh_nodes"] == 1
     with pytest.raises(ValueError, match="finished"):
         b.solid(1, 1, 1)
+
+
+# --- host logic of the round-3 kernel forms (no GPU) -------------------------------------------
+
+def _perlin_texture(sid):
+    s = rtamd.Scene(sid, 32, 24, seed=1)
+    t = next(t for t in s.textures if t.format == rtamd.scene.TEX_R32F and t.width == 6)
+    return np.frombuffer(t.data, dtype=np.float32).copy()
+
+
+@pytest.mark.parametrize("sid", [3, 5, 8])
+def test_perlin_table_packs_exactly(sid):
+    """rt_debug_perlin_pack (what rt_upload_texture keeps beside the texture and the kernel's
+    perlin_noise_pk reads): row r = (ranvec x, y, z of row r, perm x | perm y << 8 | perm z << 16),
+    so every value the reference's noise reads (texture.glsl:38-77: texelFetch, then int() of
+    the perm columns) is there unchanged."""
+    L = rtamd.amd()
+    tex = _perlin_texture(sid)
+    out = np.zeros((256, 4), np.float32)
+    assert L.rt_debug_perlin_pack(tex.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 6, 256,
+                                  out.ctypes.data, out.nbytes) == 1
+    t = tex.reshape(256, 6)
+    assert np.array_equal(out[:, :3].view(np.uint32), t[:, :3].view(np.uint32))
+    packed = out[:, 3].view(np.uint32)
+    for k in range(3):
+        assert np.array_equal((packed >> (8 * k)) & 0xFF, t[:, 3 + k].astype(np.int64))
+    assert np.all(packed >> 24 == 0)
+
+
+def test_perlin_table_that_does_not_pack_is_refused():
+    """A perm entry that is not a whole number 0..255 (or another shape) keeps the texture path."""
+    L = rtamd.amd()
+    fp = ctypes.POINTER(ctypes.c_float)
+    for bad in (3.5, -1.0, 256.0, float("nan")):
+        tex = _perlin_texture(8)
+        tex.reshape(256, 6)[17, 4] = bad
+        assert L.rt_debug_perlin_pack(tex.ctypes.data_as(fp), 6, 256, None, 0) == 0, bad
+    tex = _perlin_texture(8)
+    assert L.rt_debug_perlin_pack(tex.ctypes.data_as(fp), 6, 128, None, 0) == 0
+    assert L.rt_debug_perlin_pack(tex.ctypes.data_as(fp), 3, 512, None, 0) == 0
+
+
+@pytest.mark.parametrize("sid,lo,hi", [(0, 800, 1000), (1, 1000, 1000), (9, 1000, 1000), (5, 500, 500),
+                                       (8, 300, 499), (6, 0, 0), (2, 0, 0)])
+def test_sphere_pair_leaf_share(sid, lo, hi):
+    """The sphere-pair kernels' criterion (rt_render: >= 500 per mille of the leaves hold two
+    spheres, and the boxes not all canonical): scene 0's 485 spheres pair up (898), scenes 1, 3
+    and 9 are all sphere pairs, scene 5 exactly half; scene 8's cluster is 400 of its 1000
+    leaves (the ground boxes are the rest), the Cornell box has no sphere."""
+    L = rtamd.amd()
+    bvh = rtamd.Scene(sid, 32, 24, seed=1).buffers[1]
+    pm = ctypes.c_int(-1)
+    assert L.rt_debug_sphere_pair_leaves(ctypes.create_string_buffer(bvh, len(bvh)), len(bvh), ctypes.byref(pm)) == 0
+    assert lo <= pm.value <= hi, pm.value
