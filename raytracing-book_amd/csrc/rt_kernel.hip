@@ -571,7 +571,9 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
     // finite origin and direction: the canonical box planes equal the reference's dot products
     const bool fin = fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY &&
                      fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY;
-#pragma unroll 1
+    // both slots unrolled (the second slot's record loads can start during the first's tests):
+    // scenes 8 / 0 / 6 -0.4 / -1.2 / -1.1%, no spills at 125 VGPRs (profiles/r03_leaf_unroll_lib_ab.log)
+#pragma unroll
     for (int s = 0; s < 2; s++) {
         int ty = (int)((meta >> (16 + 4 * s)) & 0xFu);
         int ix = (int)((prims >> (16 * s)) & 0xFFFFu);
