@@ -126,12 +126,17 @@ RT_HD void g_sincos(float x, float* s_out, float* c_out) {
     float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
     float cp = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
                               4.166664568298827e-2f), z, -0.5f), z, 1.0f);
-    int q = rt_f2i(j) & 3;
-    float s, c;
-    if (q == 0)      { s = sp;  c = cp; }
-    else if (q == 1) { s = cp;  c = -sp; }
-    else if (q == 2) { s = -sp; c = -cp; }
-    else             { s = -cp; c = sp; }
+    /* quadrant q = rt_f2i(j) & 3 without branches: NaN -> -2^31 (fmaxf drops it) and
+     * j <= -2^31 give INT_MIN (q 0, as rt_f2i's 0 / INT_MIN), j >= 2147483520 gives
+     * rt_f2i's INT_MAX (q 3), the rest converts in range. */
+    const float jc = fminf(fmaxf(j, -2147483648.0f), 2147483520.0f);
+    int q = (int)jc & 3;
+    q = (j >= 2147483520.0f) ? 3 : q;
+    /* q 0..3: (s, c) = (sp, cp), (cp, -sp), (-sp, -cp), (-cp, sp) */
+    float s = (q & 1) ? cp : sp;
+    float c = (q & 1) ? -sp : cp;
+    s = (q & 2) ? -s : s;
+    c = (q & 2) ? -c : c;
     *s_out = s; *c_out = c;
 }
 RT_HD float g_sin(float x) { float s, c; g_sincos(x, &s, &c); return s; }
@@ -140,13 +145,12 @@ RT_HD float g_cos(float x) { float s, c; g_sincos(x, &s, &c); return c; }
 /* natural log: exponent/mantissa split (m in [sqrt(1/2), sqrt(2))), degree-9
  * polynomial for log(1+f), Cody–Waite ln2 split. */
 RT_HD float g_log(float x) {
-    if (!(x == x) || x < 0.0f) return rt_u2f(0x7fc00000u);
-    if (x == 0.0f) return rt_u2f(0xff800000u);
-    if (x == rt_u2f(0x7f800000u)) return x;
-    uint32_t u = rt_f2u(x);
-    int e = 0;
-    if (u < 0x00800000u) { x = x * 8388608.0f; u = rt_f2u(x); e = -23; }
-    e += (int)(u >> 23) - 126;                 /* x = m * 2^e, m in [0.5,1) */
+    /* the finite positive path on every input, the special cases selected at the end
+     * (NaN or x < 0 -> NaN, +-0 -> -inf, +inf -> +inf): no branches */
+    const uint32_t u0 = rt_f2u(x);
+    const int sub = u0 < 0x00800000u;             /* +0 and subnormals: scale by 2^23 */
+    const uint32_t u = sub ? rt_f2u(x * 8388608.0f) : u0;
+    int e = (sub ? -23 : 0) + (int)(u >> 23) - 126;   /* x = m * 2^e, m in [0.5,1) */
     float m = rt_u2f((u & 0x007fffffu) | 0x3f000000u);
     if (m < 0.707106781186547524f) { e -= 1; m = m + m - 1.0f; }
     else { m = m - 1.0f; }
@@ -160,7 +164,10 @@ RT_HD float g_log(float x) {
     y = fmaf(fe, -2.12194440e-4f, y);
     y = fmaf(-0.5f, z, y);
     float r = m + y;
-    return fmaf(fe, 0.693359375f, r);
+    r = fmaf(fe, 0.693359375f, r);
+    r = (x == rt_u2f(0x7f800000u)) ? x : r;
+    r = (x == 0.0f) ? rt_u2f(0xff800000u) : r;
+    return (!(x == x) || x < 0.0f) ? rt_u2f(0x7fc00000u) : r;
 }
 
 /* asin core on [0, 0.5]: x + x*z*P(z), z = x*x */

@@ -83,6 +83,11 @@ def test_multiframe_progressive_matches_oracle(gpu):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
+SPECIALS = np.array([np.nan, 0.0, -0.0, np.inf, -np.inf, -1.0, -1e-30, 1e-45, 1e-40, 1.1754942e-38, 1.1754944e-38,
+                     3.3732712e9, 3.3732714e9, -3.3732712e9, 1e10, -1e10, 3.4028235e38, -3.4028235e38,
+                     2.5e7, 1.6777216e7, 1e-3, 0.7071067, 0.7071068, 1.0, 2.0], np.float32)
+
+
 def test_builtins_bit_exact_on_device(gpu):
     """rt_glsl.h built-ins evaluated by gfx950 == evaluated by the x86 oracle."""
     import ctypes
@@ -92,6 +97,9 @@ def test_builtins_bit_exact_on_device(gpu):
     for name, lo, hi in [("sin", -3e5, 3e5), ("cos", -100, 100), ("log", 0, 1), ("acos", -1, 1), ("atan2", -5, 5),
                          ("fract", -1e4, 1e4), ("sqrt", 0, 1e6)]:
         x = rng.uniform(lo, hi, 20000).astype(np.float32)
+        # the branch-free special cases (rt_glsl.h g_log, g_sincos's quadrant): NaN, signed
+        # zeros and infinities, negatives, subnormals, quadrants past int range
+        x[:SPECIALS.size] = SPECIALS
         y = rng.uniform(-5, 5, 20000).astype(np.float32)
         ref = pyoracle.eval_builtin(name, x, y)
         out = np.empty_like(x)

@@ -77,6 +77,24 @@ def test_builtin_accuracy(name, fn, lo, hi, max_ulp):
     assert err.max() <= max_ulp, f"{name}: {err.max()} ulp"
 
 
+def test_builtin_special_cases():
+    """g_log's and g_sincos's special inputs (both branch-free in rt_glsl.h): NaN and x < 0 give
+    NaN, +-0 gives -inf, +inf gives +inf, subnormals are scaled into range; sin / cos of NaN and
+    of +-inf are NaN."""
+    x = np.array([np.nan, -1.0, -1e-30, 0.0, -0.0, np.inf], np.float32)
+    got = pyoracle.eval_builtin("log", x)
+    assert np.isnan(got[:3]).all() and (got[3:5] == -np.inf).all() and got[5] == np.inf
+    sub = np.array([1e-45, 1e-40, 1.1754942e-38], np.float32)
+    assert (_ulp_err(pyoracle.eval_builtin("log", sub), np.log(sub.astype(np.float64))) <= 2.0).all()
+    for name in ("sin", "cos"):
+        assert np.isnan(pyoracle.eval_builtin(name, np.array([np.nan, np.inf, -np.inf], np.float32))).all()
+        # past |x| ~ 2^20 the reduction is not accurate (defined, deterministic; the quadrant
+        # follows rt_f2i's saturation: tools/glsl_equiv.sh compares it with the branchy form)
+        big = np.array([3.3732712e9, 3.3732714e9, -3.4028235e38, 1e10], np.float32)
+        assert np.array_equal(pyoracle.eval_builtin(name, big).view(np.uint32),
+                              pyoracle.eval_builtin(name, big).view(np.uint32))
+
+
 def test_builtin_atan2_and_fract():
     rng = np.random.default_rng(8)
     y = rng.uniform(-10, 10, 100000).astype(np.float32)
