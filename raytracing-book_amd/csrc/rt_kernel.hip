@@ -391,20 +391,22 @@ __device__ __forceinline__ bool sphere_bounds(float4 A, float4 B, v3 o, v3 d, fl
         float half_b = g_dot(oc, d);
         float c = g_dot(oc, oc) - B.w * B.w;
         float disc = half_b * half_b - a * c;
-        if (disc < 0.0f) return false;
+        // without branches: disc < 0 makes sq and both roots NaN, and every test below fails
+        // as the early return did (t1 / t2 are not read on false).  All lanes take the ballot
+        // now; it only chooses between div_nr and '/', which give the same bits in its regime.
         float sq = sqrtf(disc);
         fd = fd && __ballot(!(a >= 0x1p-60f)) == 0;
         const float ra = fd ? rcp_nr(a) : 0.0f;
         float r_lo = fd ? div_nr(-half_b - sq, a, ra) : (-half_b - sq) / a;
         float r_hi = fd ? div_nr(-half_b + sq, a, ra) : (-half_b + sq) / a;
-        if (-RT_INFINITY < r_lo && r_lo < RT_INFINITY) t1 = r_lo;
-        else if (-RT_INFINITY < r_hi && r_hi < RT_INFINITY) t1 = r_hi;
-        else return false;
-        float lo2 = t1 + 0.0001f;
-        if (lo2 < r_lo && r_lo < RT_INFINITY) t2 = r_lo;
-        else if (lo2 < r_hi && r_hi < RT_INFINITY) t2 = r_hi;
-        else return false;
-        return true;
+        const bool lo_in = -RT_INFINITY < r_lo && r_lo < RT_INFINITY;
+        const bool hi_in = -RT_INFINITY < r_hi && r_hi < RT_INFINITY;
+        t1 = lo_in ? r_lo : r_hi;
+        const float lo2 = t1 + 0.0001f;
+        const bool lo_2 = lo2 < r_lo && r_lo < RT_INFINITY;
+        const bool hi_2 = lo2 < r_hi && r_hi < RT_INFINITY;
+        t2 = lo_2 ? r_lo : r_hi;
+        return !(disc < 0.0f) && (lo_in || hi_in) && (lo_2 || hi_2);
     }
 }
 
@@ -847,6 +849,15 @@ __device__ __forceinline__ void texel(const rt_dtex& T, int x, int y, float out[
         out[2] = unorm8_fast((c >> 16) & 0xFFu);
     }
 }
+// texel() at an (x, y) the caller has clamped into the image of a texture with data, without
+// branches: a float texel and an RGBA8 texel are both one 32-bit word at the same index, so one
+// load serves either and the format selects the conversion
+__device__ __forceinline__ void texel_in(const rt_dtex& T, int x, int y, float out[3]) {
+    const uint32_t c = ((__attribute__((address_space(1))) const uint32_t*)T.data)[y * T.w + x];
+    out[0] = T.is_float ? __uint_as_float(c) : unorm8_fast(c & 0xFFu);
+    out[1] = T.is_float ? 0.0f : unorm8_fast((c >> 8) & 0xFFu);
+    out[2] = T.is_float ? 0.0f : unorm8_fast((c >> 16) & 0xFFu);
+}
 __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
     float t[3];
     texel(T, x, y, t);
@@ -1048,7 +1059,7 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         x0 = x0 < 0 ? 0 : (x0 > T.w - 1 ? T.w - 1 : x0);
         y0 = y0 < 0 ? 0 : (y0 > T.h - 1 ? T.h - 1 : y0);
         float t00[3], t10[3], t01[3], t11[3];
-        texel(T, x0, y0, t00); texel(T, x1, y0, t10); texel(T, x0, y1, t01); texel(T, x1, y1, t11);
+        texel_in(T, x0, y0, t00); texel_in(T, x1, y0, t10); texel_in(T, x0, y1, t01); texel_in(T, x1, y1, t11);
         float r[3];
 #pragma unroll
         for (int c = 0; c < 3; c++)
