@@ -165,7 +165,9 @@ struct rt_ctx {
     bool fastdiv = true;   // shared-reciprocal divisions where exact (env RT_FASTDIV=0 disables; A/B)
     bool box_pretest = true;   // the canonical box tests' bounds pre-test (env RT_BOX_PRETEST=0 disables; A/B)
     int sm_batch = 64;   // render_stream's shading batch (env RT_SM_BATCH) ...
-    int sm_frac = 56;    // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC)
+    int sm_frac = 0;     // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC); 0 = by kernel:
+                         // 50 for the compact-box kernels (scene 8 1080p -1.1%, 4K -1.6% against 56), 56 else
+                         // (scene 6 +1.4% at 52; profiles/r03_sm_frac_knobs.log)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
     bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
     bool sph_lds = true;   // sphere records' first two float4 in LDS when they fit (env RT_SPH_LDS=0 disables; A/B)
@@ -1563,7 +1565,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                     : 0;
     a.variant = c->variant;
     a.sm_batch = c->sm_batch;
-    a.sm_frac = c->sm_frac;
     a.walk_frac = c->walk_frac;
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
@@ -1600,6 +1601,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.n_sph_lds = n_sph;
     a.n_box_lds = n_box;
     a.box_all_cmp = (c->compact_boxes && n_box > 0 && c->n_boxc_ok == n_box) ? 1 : 0;
+    a.sm_frac = c->sm_frac ? c->sm_frac : (a.box_all_cmp ? 50 : 56);
     // the sphere-pair kernels (rt_kernel.hip leaf_prims_t SPAIR) for a BVH whose leaves are mostly
     // two spheres (scene 0: 485 spheres); measured slower where they are not
     if (c->pair_leaves < 0) c->pair_leaves = pair_leaves_permille(c->links, c->n_dnodes);
@@ -2167,7 +2169,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
         case RT_OPTION_SM_BATCH: if (v < 1 || v > 64) return bad(); c->sm_batch = v; break;
-        case RT_OPTION_SM_FRAC: if (v < 1 || v > 64) return bad(); c->sm_frac = v; break;
+        case RT_OPTION_SM_FRAC: if (v < 0 || v > 64) return bad(); c->sm_frac = v; break;
         case RT_OPTION_WALK_FRAC: if (v < 1 || v > 64) return bad(); c->walk_frac = v; break;
         case RT_OPTION_WATCHDOG_MS: if (v < 0) return bad(); c->watchdog_ticks = (unsigned long long)v * 100000ull; break;
         case RT_OPTION_CHUNK_WAIT_MS: if (v < 0) return bad(); c->chunk_wait_ticks = (unsigned long long)v * 100000ull; break;
