@@ -25,8 +25,9 @@ The rank-0 JSON line carries
     per wave64 VALU instruction (MI355X_MICROARCH.md:54,473; the microkernel
     tools/valu_peak.hip measures the 4-waves-per-SIMD ceiling, also reported);
   * cpu_baseline: the CPU oracle (oracle/, a restatement of the reference's
-    GLSL; the reference has no CPU path) with one thread per host CPU, >= 60 s,
-    on a bounded stripe of the same workload, plus the C1 CPU config in full.
+    GLSL; the reference has no CPU path) with one thread per CPU of the job's
+    cgroup quota (else its affinity set), >= 60 s, on a bounded stripe of the
+    same workload, plus its single-thread rate and the C1 CPU config in full.
 """
 import argparse
 import json
@@ -118,6 +119,17 @@ def host_facts():
             "cgroup_cpu_quota": quota}
 
 
+def cpu_threads(facts):
+    """Threads for the CPU baseline: the CPUs this job may actually use.  One per visible CPU
+    oversubscribes a cgroup quota (256 threads in a 16-CPU quota measured ~3.5x below 16
+    threads), so the quota, rounded, when there is one, else the affinity count."""
+    n = facts.get("affinity_cpus") or facts.get("nproc") or 1
+    q = facts.get("cgroup_cpu_quota")
+    if q:
+        n = min(n, max(1, int(round(q))))
+    return max(1, int(n))
+
+
 def _oracle_rate(pyoracle, rtamd, osc, W, H, rows_rank, rows_world, stripe, seed, seconds, threads):
     """Frames of the rows of one stripe set, in growing chunks, until `seconds`."""
     image = np.zeros((H, W, 4), np.float32)
@@ -136,8 +148,8 @@ def _oracle_rate(pyoracle, rtamd, osc, W, H, rows_rank, rows_world, stripe, seed
 
 def cpu_baseline(scene, args):
     """CPU oracle (oracle/, the build's scalar restatement of compute.glsl; the
-    reference has no CPU path) on this host.  One thread per host
-    CPU, >= args.cpu_seconds on the full-width rows of stripe 0 of 8 of the same
+    reference has no CPU path) on this host.  One thread per usable
+    CPU (cpu_threads), >= args.cpu_seconds on the full-width rows of stripe 0 of 8 of the same
     workload; the rate does not depend on spp.  Also: a 1-thread rate, the C1
     config (scene 9, 400x225, 64 spp, depth 8) rendered in full, and the host
     facts (the job's cgroup CPU quota caps what many threads can get)."""
@@ -145,7 +157,7 @@ def cpu_baseline(scene, args):
     import pyoracle
     import rtamd
     facts = host_facts()
-    threads = facts["nproc"] or 1
+    threads = cpu_threads(facts)
     osc = pyoracle.OracleScene(scene, max_depth=args.depth, spp=args.spp_total)
     W, H = scene.width, scene.height
     samples, nf, rows, dt = _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 8, args.stripe_rows, args.seed,
@@ -159,22 +171,24 @@ def cpu_baseline(scene, args):
     t = time.perf_counter()
     pyoracle.render(oc1, rf, first_frame=1, nthreads=threads)
     c1_s = time.perf_counter() - t
-    eff = facts["cgroup_cpu_quota"] or facts["affinity_cpus"]
     per_thread = s1 / dt1 / 1e6
     return {
         "value": round(samples / dt / 1e6, 3),
         "unit": "Msamples/s",
-        "cores": int(round(eff)) if eff else threads,
+        "cores": threads,
         "kind": "port",
         "threads": threads,
+        "threads_rule": "round(cgroup CPU quota), else the affinity CPU count, capped by both",
         **facts,
         "sample": f"scene {args.scene} {W}x{H} max_depth {args.depth}: rows of stripe 0/8 ({rows} rows x {W}), "
                   f"{nf} frames = {samples} samples in {dt:.1f} s, {threads} threads",
         "single_thread_msamples_s": round(per_thread, 3),
-        "full_host_estimate_msamples_s": round(per_thread * facts["physical_cores"], 1)
-        if facts["physical_cores"] else None,
-        "full_host_estimate_note": "single-thread rate x physical cores (extrapolated, SMT not counted): what the "
-                                   "whole host would do without the job's cgroup CPU quota",
+        "single_thread_x_threads_msamples_s": round(per_thread * threads, 3),
+        "extrapolated_not_measured": {
+            "physical_cores_x_single_thread_msamples_s": round(per_thread * facts["physical_cores"], 1)
+            if facts["physical_cores"] else None,
+            "note": "single-thread rate x the host's physical cores: an extrapolation for a host without the "
+                    "job's CPU quota, not a measurement"},
         "c1": {"config": "scene 9 (Book-1 three spheres), 400x225, 64 spp, max_depth 8, full render",
                "samples": 400 * 225 * 64, "seconds": round(c1_s, 3),
                "msamples_s": round(400 * 225 * 64 / c1_s / 1e6, 3), "threads": threads},
@@ -301,10 +315,27 @@ def main():
     samples_total = args.width * args.height * F * args.steps   # all ranks together
     value = samples_total / t_max / 1e6
 
-    # RCCL gather of the accumulated stripes to rank 0 (reported separately, not in value)
+    # Gather of the accumulated stripes to rank 0 (reported separately, not in value): the
+    # product's path behind the C ABI first (rt_comm_init + rt_gather_image: ncclSend to rank 0,
+    # de-interleave kernel there; what a Java host calls), torch.distributed.gather as the
+    # reported fallback if that path fails (e.g. several ranks on one GPU in a rehearsal).
+    full, gather_path, gather_err = None, None, None
     torch.cuda.synchronize()
     tg = time.perf_counter()
-    full = rdist.gather_image(image, args.height, world, args.stripe_rows)
+    try:
+        full = rdist.native_gather(ctx, rank, world)
+        gather_path = "rt_gather_image (RCCL send/recv + device de-interleave)" if world > 1 \
+            else "rt_read_image (world 1)"
+    except Exception as e:   # noqa: BLE001 -- any failure of the native path falls back
+        gather_err = repr(e)[:300]
+        log("native gather failed, falling back to torch.distributed.gather:", gather_err)
+    ok = torch.tensor([0.0 if full is None and (rank == 0 or gather_err) else 1.0], dtype=torch.float64)
+    if world > 1:   # every rank takes the same path
+        ok = ok.to(f"cuda:{dev}" if torch.distributed.get_backend() == "nccl" else "cpu")
+        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+    if float(ok.item()) < 1.0:
+        full = rdist.gather_image(image, args.height, world, args.stripe_rows)
+        gather_path = "torch.distributed.gather (fallback)"
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - tg) * 1e3
 
@@ -351,6 +382,8 @@ def main():
                    "stripe_rows": args.stripe_rows, "parallelism": f"row-stripes x{world}"},
         "kernel_ms_per_launch": {"max": round(max(rank_ms), 3), "min": round(min(rank_ms), 3)},
         "gather_ms": round(gather_ms, 3),
+        "gather_path": gather_path,
+        "gather_native_error": gather_err,
         "nan_pixels": nan_px,
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -93,14 +93,33 @@ public class RtAmdRaytraceExecutor {
         completeListeners.add(l);
     }
 
-    /** One frame, as the reference's raytrace(). */
+    /** One frame, as the reference's raytrace() (unclamped, like the reference's). */
     public void raytrace() {
-        raytrace(1);
+        launch(1);
     }
 
-    /** n frames in one launch: frame_count numSamples+1 .. numSamples+n, one Math.random() each. */
-    public void raytrace(int n) {
-        if (n <= 0) return;
+    /**
+     * Up to n frames in one launch: frame_count numSamples+1 .. numSamples+k, one
+     * Math.random() each, where k = n clamped to the frames still missing from
+     * samplePerPixel (when one is set).  The reference renders exactly samplePerPixel
+     * frames, one raytrace() per loop iteration while !sampleComplete()
+     * (RaytraceExecutor.java:100-156, Window.java:250-281), so a caller queueing
+     * FRAMES_PER_DISPLAY frames at a time must not run past it: with spp 20 and 16 per
+     * display the launches are 16 then 4 (rtamd/render.py and rt_main.cpp clamp the same way).
+     * Returns the number of frames queued.
+     */
+    public int raytrace(int n) {
+        return launch(clampFrames(n, numSamples, samplePerPixel));
+    }
+
+    /** The frames raytrace(n) queues after numSamples of samplePerPixel (0 = unbounded). */
+    static int clampFrames(int n, int numSamples, int samplePerPixel) {
+        if (samplePerPixel > 0) n = Math.min(n, samplePerPixel - numSamples);
+        return Math.max(n, 0);
+    }
+
+    private int launch(int n) {
+        if (n <= 0) return 0;
         if (numSamples == 0) startMillis = System.currentTimeMillis();
         // as the reference does with its finished QueryTimers (RaytraceExecutor.java:106-115): the
         // previous call's device time once it is available, never waiting for it
@@ -112,6 +131,7 @@ public class RtAmdRaytraceExecutor {
         for (int i = 0; i < n; i++) factors[i] = (float) Math.random();
         rt.render(numSamples + 1, factors);
         numSamples += n;
+        return n;
     }
 
     public boolean sampleComplete() {

@@ -991,6 +991,18 @@ int ensure(rt_ctx* c, Device& d, DevBuf& b, size_t n) {
             return set_err(ctx, RT_ERR_DEVICE, std::string(#call) + ": " + rccl().GetErrorString(e_));    \
     } while (0)
 
+// Runs the calls between ncclGroupStart and ncclGroupEnd and closes the group whatever they
+// return, so a failed Send / Recv / copy does not leave a group open on this thread (later
+// RCCL calls would be queued into it).  The body's error wins over GroupEnd's.
+template <class F>
+int group_body(rt_ctx* c, F&& body) {
+    const int r = body();
+    const ncclResult_t e = rccl().GroupEnd();
+    if (r) return r;
+    if (e != ncclSuccess) return set_err(c, RT_ERR_DEVICE, std::string("ncclGroupEnd: ") + rccl().GetErrorString(e));
+    return RT_OK;
+}
+
 // Multi-device context: device k's stripe block (local_rows x W, in its padded slot) into
 // device 0's gather buffer, then the de-interleave kernel into device 0's full image.
 // RCCL (ncclCommInitAll over the context's devices, one ncclSend per device k > 0 and the
@@ -1019,19 +1031,23 @@ int device_gather(rt_ctx* c) {
     }
     if (d0.comm) {
         NCCLCHK(c, rccl().GroupStart());
-        for (int k = 0; k < ndev; k++) {
-            Device& d = c->devs[k];
-            const size_t n = (size_t)d.local_rows * c->width * 4;   // floats of the block
-            char* dst = (char*)d0.gather.ptr + slot * k;
-            HIPCHK(c, hipSetDevice(d.id));
-            if (k == 0) {
-                HIPCHK(c, hipMemcpyAsync(dst, d.image_ptr, n * 4, hipMemcpyDeviceToDevice, d0.stream));
-            } else if (n) {
-                NCCLCHK(c, rccl().Send(d.image_ptr, n, ncclFloat, 0, d.comm, d.stream));
-                NCCLCHK(c, rccl().Recv(dst, n, ncclFloat, k, d0.comm, d0.stream));
+        // the group is closed on every path: an error inside it is returned after GroupEnd
+        int in_group = group_body(c, [&]() -> int {
+            for (int k = 0; k < ndev; k++) {
+                Device& d = c->devs[k];
+                const size_t n = (size_t)d.local_rows * c->width * 4;   // floats of the block
+                char* dst = (char*)d0.gather.ptr + slot * k;
+                HIPCHK(c, hipSetDevice(d.id));
+                if (k == 0) {
+                    HIPCHK(c, hipMemcpyAsync(dst, d.image_ptr, n * 4, hipMemcpyDeviceToDevice, d0.stream));
+                } else if (n) {
+                    NCCLCHK(c, rccl().Send(d.image_ptr, n, ncclFloat, 0, d.comm, d.stream));
+                    NCCLCHK(c, rccl().Recv(dst, n, ncclFloat, k, d0.comm, d0.stream));
+                }
             }
-        }
-        NCCLCHK(c, rccl().GroupEnd());
+            return RT_OK;
+        });
+        if (in_group) return in_group;
         for (Device& d : c->devs) {
             HIPCHK(c, hipSetDevice(d.id));
             HIPCHK(c, hipStreamSynchronize(d.stream));
@@ -1111,13 +1127,17 @@ int rt_gather_image(rt_ctx* c, float* rgba) {
         if (ensure(c, d, d.gather, slot * world) || ensure(c, d, d.full, (size_t)c->height * c->width * 16))
             return RT_ERR_DEVICE;
         NCCLCHK(c, rccl().GroupStart());
-        HIPCHK(c, hipMemcpyAsync(d.gather.ptr, d.image_ptr, (size_t)d.local_rows * c->width * 16,
-                                 hipMemcpyDeviceToDevice, d.stream));
-        for (int k = 1; k < world; k++) {
-            const size_t nk = (size_t)local_rows_of(c->height, k, world, c->stripe_rows) * c->width * 4;
-            if (nk) NCCLCHK(c, rccl().Recv((char*)d.gather.ptr + slot * k, nk, ncclFloat, k, d.comm, d.stream));
-        }
-        NCCLCHK(c, rccl().GroupEnd());
+        int in_group = group_body(c, [&]() -> int {
+            HIPCHK(c, hipMemcpyAsync(d.gather.ptr, d.image_ptr, (size_t)d.local_rows * c->width * 16,
+                                     hipMemcpyDeviceToDevice, d.stream));
+            for (int k = 1; k < world; k++) {
+                const size_t nk = (size_t)local_rows_of(c->height, k, world, c->stripe_rows) * c->width * 4;
+                if (nk)
+                    NCCLCHK(c, rccl().Recv((char*)d.gather.ptr + slot * k, nk, ncclFloat, k, d.comm, d.stream));
+            }
+            return RT_OK;
+        });
+        if (in_group) return in_group;
         if (rt_launch_deinterleave(d.gather.ptr, d.full.ptr, c->width, c->height, world, c->stripe_rows,
                                    d.padded_rows, d.stream))
             return set_err(c, RT_ERR_DEVICE, "de-interleave kernel launch failed");
@@ -1199,7 +1219,7 @@ int rt_destroy(rt_ctx* c) {
         dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter);
         dev_free(d.tile_done); dev_free(d.samples); dev_free(d.wbuf); dev_free(d.dquads); dev_free(d.dboxes);
         dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links); dev_free(d.dboxc);
-        dev_free(d.gather); dev_free(d.full);
+        dev_free(d.gather); dev_free(d.full); dev_free(d.perlin_pk); dev_free(d.sflags);
         if (d.comm && rccl().ok) (void)rccl().CommDestroy(d.comm);
         if (d.ring) (void)hipHostFree(d.ring);
         for (auto& e : d.ring_ev)

@@ -73,6 +73,93 @@ def test_gloo_stripe_gather(world):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
 
 
+class _FakeCtx:
+    """Stands in for rtamd.RenderContext in the native gather's host logic (no GPU here)."""
+
+    def __init__(self, rank, image=None):
+        self.rank, self.image, self.uid, self.calls = rank, image, None, []
+
+    def read_image(self):
+        self.calls.append("read_image")
+        return self.image
+
+    def comm_init(self, uid, rank, world):
+        self.calls.append(("comm_init", rank, world))
+        self.uid = bytes(uid)
+
+    def gather_image(self):
+        self.calls.append("gather_image")
+        return self.image if self.rank == 0 else None
+
+
+def test_native_gather_world1_is_read_image():
+    """at world 1 the C-ABI gather (bench.py's gather path) is rt_read_image."""
+    img = np.random.default_rng(1).random((7, 5, 4), dtype=np.float32)
+    c = _FakeCtx(0, img)
+    out = rdist.native_gather(c, 0, 1)
+    assert out is img and c.calls == ["read_image"]
+
+
+def _native_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        rdist.init_from_env(backend="gloo")
+        import rtamd.render as R
+
+        def fake_uid():
+            assert rank == 0, "only rank 0 makes the communicator id"
+            return bytes(range(7, 7 + 128))
+        R.comm_unique_id = fake_uid
+        c = _FakeCtx(rank, np.full((3, 2, 4), 5.0, np.float32) if rank == 0 else None)
+        out = rdist.native_gather(c, rank, world)
+        q.put((rank, c.uid, c.calls, None if out is None else out.shape))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report, never hang the parent
+        q.put(("error", f"rank {rank}: {e!r}"))
+
+
+def test_native_gather_hands_rank0_id_to_every_rank():
+    """The native gather's host side at world 2 (gloo): rank 0 makes the RCCL id, torch.distributed
+    broadcasts it, every rank runs rt_comm_init(id, rank, world) then rt_gather_image; only rank 0
+    returns an image."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not q.empty():
+        msgs.append(q.get())
+    assert len(msgs) == world and all(m[0] != "error" for m in msgs), msgs
+    by_rank = {m[0]: m for m in msgs}
+    uid = bytes(range(7, 7 + 128))
+    for r in range(world):
+        _, got, calls, shape = by_rank[r]
+        assert got == uid and calls == [("comm_init", r, world), "gather_image"], (r, calls)
+        assert shape == ((3, 2, 4) if r == 0 else None)
+
+
+def test_bench_cpu_threads_follow_the_quota():
+    """the CPU baseline uses the job's CPUs (cgroup quota, else affinity), not nproc."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.cpu_threads({"nproc": 256, "affinity_cpus": 256, "cgroup_cpu_quota": 16.0}) == 16
+    assert bench.cpu_threads({"nproc": 256, "affinity_cpus": 8, "cgroup_cpu_quota": 16.0}) == 8
+    assert bench.cpu_threads({"nproc": 256, "affinity_cpus": 12, "cgroup_cpu_quota": None}) == 12
+    assert bench.cpu_threads({"nproc": 4, "affinity_cpus": 4, "cgroup_cpu_quota": 0.4}) == 1
+
+
 def test_gather_single_rank_is_identity():
     block = torch.from_numpy(np.random.default_rng(0).random((16, 5, 4), dtype=np.float32))
     img = rdist.gather_image(block, 13, 1, 16)

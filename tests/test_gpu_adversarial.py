@@ -159,3 +159,28 @@ def test_release_library_has_no_ab_options(gpu):
         with pytest.raises(rtamd.RTError, match="unknown option"):
             ctx.set_option(name, 0)
     ctx.close()
+
+
+def test_shading_threshold_by_kernel(gpu):
+    """sm_frac 0 (the default) picks the threshold by kernel (50/64 for the compact-box kernels,
+    56/64 else, rt_capi.hip); explicit values 1..64 override it and anything else is refused.
+    The threshold only regroups which lanes shade together: scene 8 (compact boxes) and scene 6
+    render the same bits at 0, 50 and 56."""
+    ctx = rtamd.RenderContext()
+    assert ctx.get_option("sm_frac") == 0
+    for v in (-1, 65):
+        with pytest.raises(rtamd.RTError, match="out of range"):
+            ctx.set_option("sm_frac", v)
+    ctx.close()
+    for sid in (8, 6):
+        scene = rtamd.Scene(sid, 160, 96, seed=1)
+        imgs = []
+        for v in (0, 50, 56):
+            c = rtamd.RenderContext(options={"sm_frac": v})
+            c.upload_scene(scene)
+            c.set_params(max_depth=5, spp=4096)
+            c.resize(160, 96)
+            c.render(1, rtamd.frame_rand_factors(1, 0, 8))
+            imgs.append(c.read_image())
+            c.close()
+        assert bit_equal(imgs[0], imgs[1]) and bit_equal(imgs[0], imgs[2]), f"scene {sid}"

@@ -147,3 +147,23 @@ def test_lds_record_copies_change_no_bit_1080p(gpu, knob, sid):
     on = render(scene, 8, 5, 4096)
     off = render(scene, 8, 5, 4096, options={knob: 0})
     assert bit_equal(on, off), mismatch_report(on, off)
+
+
+# Walk structure / scheduling options against the default, whole 1080p images of 8 frames
+# (the small-image suite once passed a walk that diverged at full size, so
+# every non-default walk or scheduling form is gated here, bit for bit).
+WALK_OPTIONS = [
+    ("sm_frac", {"sm_frac": 8}), ("sm_frac", {"sm_frac": 64}), ("sm_batch", {"sm_batch": 16}),
+    ("walk_frac", {"walk_frac": 16}), ("walk_frac", {"walk_frac": 64}),
+    ("sphere_pairs", {"sphere_pairs": 0}), ("spine", {"spine": 0}),
+    ("two_level", {"lds_node_cap": 16384}), ("two_level_leaf_global", {"lds_node_cap": 16384, "tl_leaf_lds": 0}),
+]
+
+
+@pytest.mark.parametrize("sid", [8, 0])
+@pytest.mark.parametrize("name,opts", WALK_OPTIONS, ids=[f"{n}-{list(o.values())[-1]}" for n, o in WALK_OPTIONS])
+def test_walk_and_schedule_options_change_no_bit_1080p(gpu, sid, name, opts):
+    scene = rtamd.Scene(sid, 1920, 1080, seed=1)
+    base = render(scene, 8, 5, 4096)
+    other = render(scene, 8, 5, 4096, options=opts)
+    assert bit_equal(base, other), f"{name} {opts}: " + mismatch_report(base, other)

@@ -148,6 +148,62 @@ def test_executor_polls_dispatch_time_without_waiting():
     """getLastDispatchTime refreshes on every raytrace() from the previous render's device time
     when it is ready (rt_render_done), as the reference polls its finished timer queries."""
     src = open(os.path.join(JAVA, "RtAmdRaytraceExecutor.java")).read()
-    body = src[src.index("public void raytrace(int n)"):]
-    body = body[:body.index("\n    }\n")]
+    body = _java_method(src, "private int launch(int n)")
     assert "rt.renderDoneNanos()" in body and "lastDispatchTime" in body
+
+
+def _java_method(src, signature):
+    body = src[src.index(signature):]
+    return body[:body.index("\n    }\n")]
+
+
+def _clamp_frames_py(src):
+    """RtAmdRaytraceExecutor.clampFrames translated statement by statement into Python (its
+    body is two Java statements over ints: an if with Math.min, then a return of Math.max)."""
+    body = _java_method(src, "static int clampFrames(int n, int numSamples, int samplePerPixel)")
+    stmts = [s.strip() for s in body.split("{", 1)[1].split(";") if s.strip()]
+    assert len(stmts) == 2, stmts
+    m = re.fullmatch(r"if \((\w+ > 0)\) n = Math\.min\((.+)\)", stmts[0])
+    assert m, stmts[0]
+    r = re.fullmatch(r"return Math\.max\((.+)\)", stmts[1])
+    assert r, stmts[1]
+    py = (f"def clamp(n, numSamples, samplePerPixel):\n"
+          f"    if {m.group(1)}: n = min({m.group(2)})\n"
+          f"    return max({r.group(1)})\n")
+    ns = {}
+    exec(py, ns)
+    return ns["clamp"]
+
+
+def test_dropin_renders_exactly_sample_per_pixel():
+    """the patched Window loop calls raytrace(FRAMES_PER_DISPLAY) while
+    !sampleComplete(); the reference renders exactly samplePerPixel frames (RaytraceExecutor.java:
+    100-156, Window.java:250-281; CLI default 20, Main.java:36).  raytrace(int) clamps to the
+    frames still missing, so with spp 20 and 16 frames per display the launches are 16 then 4."""
+    src = open(os.path.join(JAVA, "RtAmdRaytraceExecutor.java")).read()
+    pub = _java_method(src, "public int raytrace(int n)")
+    assert "launch(clampFrames(n, numSamples, samplePerPixel))" in pub
+    assert "launch(1)" in _java_method(src, "public void raytrace()")   # unclamped, as the reference
+    clamp = _clamp_frames_py(src)
+    win = _patch_files()["net/bowen/gui/Window.java"]["+"]
+    per_display = int(re.search(r'getInteger\("rtamd.framesPerDisplay", (\d+)\)', "\n".join(win)).group(1))
+    assert any("if (!raytraceExecutor.sampleComplete())" in l for l in win)
+    assert any("raytraceExecutor.raytrace(FRAMES_PER_DISPLAY);" in l for l in win)
+
+    def loop(spp, per):
+        num, calls = 0, []
+        while not num >= spp:               # sampleComplete(): numSamples >= samplePerPixel
+            k = clamp(per, num, spp)
+            assert k > 0
+            calls.append(k)
+            num += k
+        return calls, num
+
+    assert per_display == 16
+    assert loop(20, per_display) == ([16, 4], 20)
+    for spp in (1, 15, 16, 17, 32, 33, 4096):
+        for per in (1, 7, 16, 64):
+            calls, num = loop(spp, per)
+            assert num == spp and all(c <= per for c in calls), (spp, per, calls)
+    assert clamp(16, 20, 20) == 0 and clamp(16, 25, 20) == 0      # nothing past spp
+    assert clamp(16, 100, 0) == 16 and clamp(-3, 0, 20) == 0       # unbounded; non-positive n
