@@ -162,8 +162,9 @@ def cpu_baseline(scene, args):
     W, H = scene.width, scene.height
     samples, nf, rows, dt = _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 8, args.stripe_rows, args.seed,
                                          args.cpu_seconds, threads)
-    s1, nf1, rows1, dt1 = _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 64, args.stripe_rows, args.seed,
-                                       min(10.0, args.cpu_seconds), 1)
+    # one thread on the same rows (stripe 0 of 8), so that the two rates compare like for like
+    s1, nf1, rows1, dt1 = _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 8, args.stripe_rows, args.seed,
+                                       min(15.0, args.cpu_seconds), 1)
     # C1 (BASELINE.json configs[0]): the CPU reference path's own config, in full
     c1 = rtamd.Scene(9, 400, 225, seed=args.seed)
     oc1 = pyoracle.OracleScene(c1, max_depth=8, spp=64)
@@ -183,7 +184,9 @@ def cpu_baseline(scene, args):
         "sample": f"scene {args.scene} {W}x{H} max_depth {args.depth}: rows of stripe 0/8 ({rows} rows x {W}), "
                   f"{nf} frames = {samples} samples in {dt:.1f} s, {threads} threads",
         "single_thread_msamples_s": round(per_thread, 3),
+        "single_thread_sample": f"the same rows, {nf1} frames = {s1} samples in {dt1:.1f} s, 1 thread",
         "single_thread_x_threads_msamples_s": round(per_thread * threads, 3),
+        "parallel_efficiency": round(samples / dt / 1e6 / (per_thread * threads), 3),
         "extrapolated_not_measured": {
             "physical_cores_x_single_thread_msamples_s": round(per_thread * facts["physical_cores"], 1)
             if facts["physical_cores"] else None,

@@ -2089,12 +2089,31 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     uint2 lf;
                     if (gleaf) lf = ldg_u2(gleaves + (nx & 0x7FFFFFFFu));
                     else lf = leaves[nx & 0x7FFFFFFFu];
-                    leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0>(P, lf.x << 16, lf.y, S.o, S.d, inv, a,
-                                                                             S.time, 0.001f, tmax, S.rf,
-                                                  fx, fy, h, has, st);
+                    // Per-type deferral (P.leaf_defer = k > 0): the wave runs one block per prim type
+                    // its lanes' leaves hold, so a type held by few lanes costs a whole block for
+                    // them.  This round tests only the leaves whose every type is held by >= k of
+                    // the lanes at a leaf; a lane holding another leaf keeps it (nx unchanged: its
+                    // walk does not move) and tests it in a later round.  A lane's own tests, its
+                    // ray_t updates and its medium rand() draws keep their order, so its bits
+                    // cannot change.  When no leaf qualifies, every lane tests its leaf (progress).
+                    bool run = true;
+                    if (P.leaf_defer > 0) {
+                        const uint32_t tys = ((1u << (lf.x & 0xFu)) | (1u << ((lf.x >> 4) & 0xFu))) & 0x1Eu;
+                        uint32_t sel = 0;
+#pragma unroll
+                        for (int ty = 1; ty <= 4; ty++)
+                            if (__popcll(__ballot((tys >> ty) & 1u)) >= P.leaf_defer) sel |= 1u << ty;
+                        run = (tys & ~sel) == 0u;
+                        if (__ballot(run) == 0) run = true;
+                    }
+                    if (run) {
+                        leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0>(P, lf.x << 16, lf.y, S.o, S.d, inv,
+                                                                                 a, S.time, 0.001f, tmax, S.rf, fx,
+                                                                                 fy, h, has, st);
+                        nx = lf.x >> 8;   // the leaf's skip node
+                        if (nx == RT_LINK_NEXT_END) status = RT_SM_HIT;
+                    }
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-                    nx = lf.x >> 8;   // the leaf's skip node
-                    if (nx == RT_LINK_NEXT_END) status = RT_SM_HIT;
                 }
             }
         }

@@ -1,6 +1,6 @@
 """Run the diagnostic stats build of the render kernel and print where wave time
 goes (s_memtime per region, once per wave) and each region's SIMD lane use.
-usage: python tools/kernel_stats.py [--scene 8] [--frames 16] [--width 1920 --height 1080]"""
+usage: python tools/kernel_stats.py [--scene 8] [--frames 16] [--width 1920 --height 1080] [--options JSON]"""
 import argparse
 import ctypes
 import os
@@ -25,9 +25,11 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--options", default="{}", help='JSON, e.g. {"leaf_defer": 16}')
     a = ap.parse_args()
+    import json
     scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
-    ctx = rtamd.RenderContext(devices=(0,), ab=True)   # the stats kernels are in the A/B build
+    ctx = rtamd.RenderContext(devices=(0,), ab=True, options=json.loads(a.options) or None)   # the stats kernels are in the A/B build
     ctx.upload_scene(scene)
     ctx.set_params(max_depth=a.depth, spp=4096)
     ctx.resize(a.width, a.height)
