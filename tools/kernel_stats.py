@@ -15,7 +15,7 @@ NAMES = ["TOTAL", "START_CYC", "START_IT", "START_LN", "NODE_CYC", "NODE_IT", "N
          "QUAD_IT", "BOX_IT", "MED_IT", "FAST_TRACES", "FAST_EXACT"] + [f"FAST_WHY{r}" for r in range(1, 10)] + [
          "FAST_STEPS", "FAST_TESTS", "FAST_PRE_CYC", "FAST_POST_CYC", "FAST_EXACT_CYC",
          "SPH_CYC", "QUAD_CYC", "BOX_CYC", "MED_CYC", "TRACE_IT", "TRACE_LN", "ROUND_IT", "ROUND_LN",
-         "RET_IT", "RET_LN"]
+         "RET_IT", "RET_LN", "SPH_SM", "QUAD_SM", "BOX_SM", "MED_SM", "NODE_SM"]
 
 
 def main():
