@@ -106,12 +106,6 @@ enum {
                                            exactly zero, plus a flag byte per sample (1)    */
     RT_OPTION_SPHERE_PAIRS = 19,        /* kernels testing a two-sphere leaf's spheres at
                                            once, when most leaves are such pairs (1)        */
-    RT_OPTION_LEAF_DEFER = 20,          /* a walk round tests only the leaves whose prim
-                                           types >= this many lanes hold; the others keep
-                                           their leaf for a later round (0 = every leaf)     */
-    RT_OPTION_LANE_PAD = 21,            /* leaf-stage sphere / quad / box blocks that fewer
-                                           lanes need run on this many, results discarded
-                                           on the padding lanes (0 = off)                   */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

@@ -169,8 +169,6 @@ struct rt_ctx {
                          // 50 for the compact-box kernels (scene 8 1080p -1.1%, 4K -1.6% against 56), 56 else
                          // (scene 6 +1.4% at 52; profiles/r03_sm_frac_knobs.log)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
-    int lane_pad = 0;    // render_stream: leaf-stage blocks needed by fewer lanes run on this many (0: off)
-    int leaf_defer = 0;  // render_stream: a round tests only the leaves whose prim types this many lanes hold (0: all)
     bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
     bool sph_lds = true;   // sphere records' first two float4 in LDS when they fit (env RT_SPH_LDS=0 disables; A/B)
     bool compact_boxes = true;   // boxes' compact records when every box has one (box_test_compact; option 0: A/B)
@@ -1188,8 +1186,6 @@ int rt_create(int n_devices, const int* device_ids, rt_ctx** out) {
     if (const char* v = std::getenv("RT_SM_BATCH")) c->sm_batch = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SM_FRAC")) c->sm_frac = std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_WALK_FRAC")) c->walk_frac = std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RT_LANE_PAD")) c->lane_pad = std::max(0, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("RT_LEAF_DEFER")) c->leaf_defer = std::max(0, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("RT_SPH_LDS")) c->sph_lds = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_BIG_WG")) c->big_wg = std::atoi(v) != 0;
     if (const char* v = std::getenv("RT_COMPACT_BOXES")) c->compact_boxes = std::atoi(v) != 0;
@@ -1590,8 +1586,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.variant = c->variant;
     a.sm_batch = c->sm_batch;
     a.walk_frac = c->walk_frac;
-    a.leaf_defer = c->leaf_defer;
-    a.lane_pad = c->lane_pad;
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);
@@ -2197,8 +2191,6 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SM_BATCH: if (v < 1 || v > 64) return bad(); c->sm_batch = v; break;
         case RT_OPTION_SM_FRAC: if (v < 0 || v > 64) return bad(); c->sm_frac = v; break;
         case RT_OPTION_WALK_FRAC: if (v < 1 || v > 64) return bad(); c->walk_frac = v; break;
-        case RT_OPTION_LEAF_DEFER: if (v < 0 || v > 64) return bad(); c->leaf_defer = v; break;
-        case RT_OPTION_LANE_PAD: if (v < 0 || v > 64) return bad(); c->lane_pad = v; break;
         case RT_OPTION_WATCHDOG_MS: if (v < 0) return bad(); c->watchdog_ticks = (unsigned long long)v * 100000ull; break;
         case RT_OPTION_CHUNK_WAIT_MS: if (v < 0) return bad(); c->chunk_wait_ticks = (unsigned long long)v * 100000ull; break;
         case RT_OPTION_LDS_NODE_CAP: if (v < 0) return bad(); c->lds_node_cap = v; break;
@@ -2233,8 +2225,6 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_SM_BATCH: *v = c->sm_batch; break;
         case RT_OPTION_SM_FRAC: *v = c->sm_frac; break;
         case RT_OPTION_WALK_FRAC: *v = c->walk_frac; break;
-        case RT_OPTION_LEAF_DEFER: *v = c->leaf_defer; break;
-        case RT_OPTION_LANE_PAD: *v = c->lane_pad; break;
         case RT_OPTION_WATCHDOG_MS: *v = (int)std::min<unsigned long long>(INT_MAX, c->watchdog_ticks / 100000ull); break;
         case RT_OPTION_CHUNK_WAIT_MS: *v = (int)std::min<unsigned long long>(INT_MAX, c->chunk_wait_ticks / 100000ull); break;
         case RT_OPTION_LDS_NODE_CAP: *v = c->lds_node_cap; break;

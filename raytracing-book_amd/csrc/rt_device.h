@@ -120,11 +120,6 @@ struct rt_kernel_args {
     int sm_frac;                 // or this many 64ths of the lanes with a walk (or none runs)
     int walk_frac;               // render_sm: a round's node walk stops once this many 64ths of its lanes
                                  // hold a leaf or ended (64: all of them)
-    int lane_pad;                // > 0: the leaf stage's sphere / quad / box blocks that 1 .. lane_pad-1
-                                 // lanes need run on lane_pad lanes (rt_kernel.hip pad_join); 0: off
-    int leaf_defer;              // render_stream: > 0: a round tests only the leaves whose every prim type is
-                                 // held by at least this many of the wave's lanes at a leaf (the others keep
-                                 // their leaf for a later round); 0: every leaf
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)

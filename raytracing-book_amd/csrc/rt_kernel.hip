@@ -91,8 +91,8 @@ enum {
     // render_stream rounds: lanes of the wave idle (no sample to claim: the tail of the launch)
     ST_RET_IT, ST_RET_LN,
     // wave executions with 1..8 active lanes (a wave64 VALU instruction with <= 8 exec lanes
-    // occupies the SIMD 1.4-5x longer than with >= 9: tools/exec_ops.hip): the leaf slots' type
-    // blocks (real lanes only) and the node steps
+    // occupies the SIMD 1.4-5x longer than with >= 9 in a register-only loop: tools/exec_ops.hip):
+    // the leaf slots' type blocks and the node steps
     ST_SPH_SM, ST_QUAD_SM, ST_BOX_SM, ST_MED_SM, ST_NODE_SM, ST_N
 };
 __device__ __forceinline__ bool first_active_lane() {
@@ -120,25 +120,6 @@ __device__ __forceinline__ void st_pred(unsigned long long* st, bool pred, int i
 __device__ __forceinline__ void st_small(unsigned long long* st, bool pred, int slot) {
     const int n = __popcll(__ballot(pred));
     if (n > 0 && n <= 8 && first_active_lane()) atomicAdd(&st[slot], 1ull);
-}
-
-// ------------------------------------------------------------- lane padding
-// A wave64 VALU instruction whose exec mask has 1..8 lanes occupies its SIMD-32 far longer than
-// one with 9 or more: v_fma_f32 11.1 vs 3.4 cycles, v_max_f32 19.8 vs 4.3, v_sqrt_f32 41.8 vs
-// 8.3, v_add_f32 3.7 vs 2.5 at 4 waves per SIMD (tools/exec_ops.hip, profiles/r04_exec_ops.log),
-// with no cliff between 9 and 64.  So a side-effect-free block that only a few lanes need is
-// cheaper run on more lanes: pad_join picks, for a block that 0 < n < k lanes need
-// (k = P.lane_pad), the k - n lowest other active lanes to run it too, on a real lane's record
-// (ix of the first lane that needs it, so every address is valid), with their results
-// discarded.  Nothing a padding lane computes is kept, so no result can change.
-__device__ __forceinline__ bool pad_join(bool mine, int k, int ix, int& ix_pad) {
-    const unsigned long long m = __ballot(mine);
-    const int n = __popcll(m);
-    if (n == 0 || n >= k) return false;   // wave-uniform
-    const unsigned long long cand = __ballot(!mine);
-    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(cand >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)cand, 0u));
-    ix_pad = __builtin_amdgcn_readlane(ix, (int)__builtin_ctzll(m));
-    return !mine && rank < (unsigned)(k - n);
 }
 
 // ------------------------------------------------------------------ rand()
@@ -612,8 +593,6 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             st_pred(st, ty == RT_MODEL_QUAD, ST_QUAD_IT, ST_QUAD_LN);
             st_pred(st, ty == RT_MODEL_BOX, ST_BOX_IT, ST_BOX_LN);
             st_pred(st, ty == RT_MODEL_CONSTANT_MEDIUM, ST_MED_IT, ST_MED_LN);
-        }
-        if (STATS) {
             st_small(st, ty == RT_MODEL_SPHERE, ST_SPH_SM);
             st_small(st, ty == RT_MODEL_QUAD, ST_QUAD_SM);
             st_small(st, ty == RT_MODEL_BOX, ST_BOX_SM);
@@ -622,47 +601,22 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
         float t = 0.0f, al = 0.0f, be = 0.0f;
         int face = 0;
         bool hit = false;
-        // padding lanes (pad_join) for the pure tests: they run the block on another lane's prim
-        // and keep nothing (each block commits only for its own type)
-        bool ps = false, pq = false, pb = false;
-        int js = ix, jq = ix, jb = ix;
-        if (P.lane_pad > 0) {   // wave-uniform
-            ps = pad_join(ty == RT_MODEL_SPHERE, P.lane_pad, ix, js);
-            pq = pad_join(ty == RT_MODEL_QUAD, P.lane_pad, ix, jq);
-            pb = pad_join(ty == RT_MODEL_BOX, P.lane_pad, ix, jb);
-        }
         unsigned long long c0 = STATS ? clock64() : 0;
-        if (ty == RT_MODEL_SPHERE || ps) {
-            const int j = ps ? js : ix;
-            float ts = 0.0f;
-            bool hh;
+        if (ty == RT_MODEL_SPHERE) {
             if (P.sph_lds >= 0) {   // the record's intersection half from LDS (render_persistent)
-                const float4* r = rt_dyn_lds + P.sph_lds + 2 * j;
-                hh = sphere_t_ab(r[0], r[1], time, o, d, a, tmin, tmax, ts, fd, fd ? rcp_nr(a) : 0.0f);
+                const float4* r = rt_dyn_lds + P.sph_lds + 2 * ix;
+                hit = sphere_t_ab(r[0], r[1], time, o, d, a, tmin, tmax, t, fd, fd ? rcp_nr(a) : 0.0f);
             } else {
-                hh = sphere_t(reinterpret_cast<const float4*>(P.spheres + j), time, o, d, a, tmin, tmax, ts, fd,
-                              fd ? rcp_nr(a) : 0.0f);
+                hit = sphere_t(reinterpret_cast<const float4*>(P.spheres + ix), time, o, d, a, tmin, tmax, t, fd,
+                               fd ? rcp_nr(a) : 0.0f);
             }
-            if (!ps) {
-                hit = hh;
-                t = ts;
-                if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
-            }
+            if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
             if (STATS) st_add(st, ST_SPH_CYC, clock64() - c0);
-        }
-        if (ty == RT_MODEL_QUAD || pq) {
-            const int j = pq ? jq : ix;
-            float tq = 0.0f, aq = 0.0f, bq = 0.0f;
-            const bool hh = quad_test(P.dquads + RT_DFACE_F4 * j, o, d, tmin, tmax, tq, aq, bq, fd);
-            if (!pq) {
-                hit = hh;
-                t = tq;
-                if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = aq; h.uv_b = bq; }
-            }
+        } else if (ty == RT_MODEL_QUAD) {
+            hit = quad_test(P.dquads + RT_DFACE_F4 * ix, o, d, tmin, tmax, t, al, be, fd);
+            if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_QUAD_CYC, clock64() - c0);
-        }
-        if (ty == RT_MODEL_BOX || pb) {
-            const int j = pb ? jb : ix;
+        } else if (ty == RT_MODEL_BOX) {
             // the box's 48-byte record (rt_capi.hip compact_box), from LDS when staged: its bounds
             // for the pre-test, and -- every box of the scene having Box.java's axis-aligned
             // layout (BOXC) -- everything its faces' tests read (box_test_compact); otherwise the
@@ -671,12 +625,12 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             // plane t or its alpha / beta is then inf or NaN), so BOXC needs no finiteness check.
             float4 r0, r1, r2;
             if (P.box_cmp_lds >= 0) {
-                const float4* cr = rt_dyn_lds + P.box_cmp_lds + RT_BOXC_F4 * j;
+                const float4* cr = rt_dyn_lds + P.box_cmp_lds + RT_BOXC_F4 * ix;
                 r0 = cr[0];
                 r1 = cr[1];
                 r2 = cr[2];
             } else {
-                const float4* cr = P.dboxc + RT_BOXC_F4 * j;
+                const float4* cr = P.dboxc + RT_BOXC_F4 * ix;
                 r0 = ldg(cr);
                 r1 = ldg(cr + 1);
                 r2 = ldg(cr + 2);
@@ -689,24 +643,15 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
                 maybe = aabb_pk(make_float4(r0.x - m, r0.w + m, r0.y - m, r1.x + m),
                                 make_float4(r0.z - m, r1.y + m, 0.0f, 0.0f), o, inv, tmin, tmax);
             }
-            bool hh = false;
-            float tb = 0.0f, ab = 0.0f, bb = 0.0f;
-            int fb = 0;
             if (maybe) {
                 if constexpr (BOXC)
-                    hh = box_test_compact(r0, r1, r2, o, d, tmin, tmax, tb, fb, ab, bb, fd);
+                    hit = box_test_compact(r0, r1, r2, o, d, tmin, tmax, t, face, al, be, fd);
                 else
-                    hh = box_test(P.dboxes + RT_DBOX_F4 * j, o, d, tmin, tmax, tb, fb, ab, bb, fd);
+                    hit = box_test(P.dboxes + RT_DBOX_F4 * ix, o, d, tmin, tmax, t, face, al, be, fd);
             }
-            if (!pb) {
-                hit = hh;
-                t = tb;
-                face = fb;
-                if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = ab; h.uv_b = bb; }
-            }
+            if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
-        }
-        if (ty == RT_MODEL_CONSTANT_MEDIUM) {
+        } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
             hit = medium_test<FD>(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
             if (STATS) st_add(st, ST_MED_CYC, clock64() - c0);
         }
@@ -2160,31 +2105,12 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     uint2 lf;
                     if (gleaf) lf = ldg_u2(gleaves + (nx & 0x7FFFFFFFu));
                     else lf = leaves[nx & 0x7FFFFFFFu];
-                    // Per-type deferral (P.leaf_defer = k > 0): the wave runs one block per prim type
-                    // its lanes' leaves hold, so a type held by few lanes costs a whole block for
-                    // them.  This round tests only the leaves whose every type is held by >= k of
-                    // the lanes at a leaf; a lane holding another leaf keeps it (nx unchanged: its
-                    // walk does not move) and tests it in a later round.  A lane's own tests, its
-                    // ray_t updates and its medium rand() draws keep their order, so its bits
-                    // cannot change.  When no leaf qualifies, every lane tests its leaf (progress).
-                    bool run = true;
-                    if (P.leaf_defer > 0) {
-                        const uint32_t tys = ((1u << (lf.x & 0xFu)) | (1u << ((lf.x >> 4) & 0xFu))) & 0x1Eu;
-                        uint32_t sel = 0;
-#pragma unroll
-                        for (int ty = 1; ty <= 4; ty++)
-                            if (__popcll(__ballot((tys >> ty) & 1u)) >= P.leaf_defer) sel |= 1u << ty;
-                        run = (tys & ~sel) == 0u;
-                        if (__ballot(run) == 0) run = true;
-                    }
-                    if (run) {
-                        leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0>(P, lf.x << 16, lf.y, S.o, S.d, inv,
-                                                                                 a, S.time, 0.001f, tmax, S.rf, fx,
-                                                                                 fy, h, has, st);
-                        nx = lf.x >> 8;   // the leaf's skip node
-                        if (nx == RT_LINK_NEXT_END) status = RT_SM_HIT;
-                    }
+                    leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0>(P, lf.x << 16, lf.y, S.o, S.d, inv, a,
+                                                                             S.time, 0.001f, tmax, S.rf,
+                                                  fx, fy, h, has, st);
                     if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+                    nx = lf.x >> 8;   // the leaf's skip node
+                    if (nx == RT_LINK_NEXT_END) status = RT_SM_HIT;
                 }
             }
         }

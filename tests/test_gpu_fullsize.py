@@ -156,8 +156,6 @@ WALK_OPTIONS = [
     ("sm_frac", {"sm_frac": 8}), ("sm_frac", {"sm_frac": 64}), ("sm_batch", {"sm_batch": 16}),
     ("walk_frac", {"walk_frac": 16}), ("walk_frac", {"walk_frac": 64}),
     ("sphere_pairs", {"sphere_pairs": 0}), ("spine", {"spine": 0}),
-    ("leaf_defer", {"leaf_defer": 8}), ("leaf_defer", {"leaf_defer": 24}), ("leaf_defer", {"leaf_defer": 64}),
-    ("lane_pad", {"lane_pad": 9}), ("lane_pad", {"lane_pad": 64}),
     ("two_level", {"lds_node_cap": 16384}), ("two_level_leaf_global", {"lds_node_cap": 16384, "tl_leaf_lds": 0}),
 ]
 

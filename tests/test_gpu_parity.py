@@ -48,33 +48,6 @@ def test_perlin_table_forms_match_oracle(gpu, scene_id, packed):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
-@pytest.mark.parametrize("scene_id", [8, 0, 6, 7])
-@pytest.mark.parametrize("k", [0, 1, 8, 16, 40, 64])
-def test_leaf_deferral_matches_oracle(gpu, scene_id, k):
-    """Per-type leaf deferral (rt_kernel.hip render_stream, option leaf_defer = k): a walk round
-    tests only the leaves whose prim types >= k lanes hold, the others keep their leaf.  Every k
-    (1 = no deferral in effect, 64 = defer unless every lane at a leaf agrees) bit for bit
-    against the oracle; scenes 8 (boxes, spheres, media), 0 (sphere pairs), 6 / 7 (quads,
-    rotated boxes, a medium in 7)."""
-    s = rtamd.Scene(scene_id, 48, 27, seed=1)
-    ref = oracle_image(s, 6, max_depth=5)
-    out = gpu_image(s, 6, max_depth=5, options={"leaf_defer": k})
-    assert bit_equal(out, ref), mismatch_report(out, ref)
-
-
-@pytest.mark.parametrize("scene_id", [8, 0, 6, 7, 5])
-@pytest.mark.parametrize("k", [9, 16, 64])
-def test_lane_padding_matches_oracle(gpu, scene_id, k):
-    """Lane padding (rt_kernel.hip pad_join, option lane_pad = k): a leaf-stage sphere / quad /
-    box block that 1..k-1 lanes need runs on k lanes, the padding lanes testing a real lane's
-    prim with their own ray and keeping nothing.  Bit for bit against the oracle, k = 9 (the
-    exec-lane cliff), 16 and 64 (every active lane joins)."""
-    s = rtamd.Scene(scene_id, 48, 27, seed=1)
-    ref = oracle_image(s, 6, max_depth=5)
-    out = gpu_image(s, 6, max_depth=5, options={"lane_pad": k})
-    assert bit_equal(out, ref), mismatch_report(out, ref)
-
-
 @pytest.mark.parametrize("scene_id,pairs", [(0, 1), (1, 1), (9, 1), (8, 0), (6, 0)])
 def test_sphere_pair_kernel_matches_oracle(gpu, scene_id, pairs):
     """Scenes whose leaves are mostly two spheres take the kernels that test both at once
