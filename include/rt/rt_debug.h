@@ -106,6 +106,9 @@ enum {
                                            exactly zero, plus a flag byte per sample (1)    */
     RT_OPTION_SPHERE_PAIRS = 19,        /* kernels testing a two-sphere leaf's spheres at
                                            once, when most leaves are such pairs (1)        */
+    RT_OPTION_LEAF_PREFETCH = 20,       /* compact-box kernels: each leaf slot's record loaded
+                                           before the prim-type blocks when spheres, boxes
+                                           and media are all staged in LDS (1)              */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

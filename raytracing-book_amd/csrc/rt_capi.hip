@@ -168,6 +168,7 @@ struct rt_ctx {
     int sm_frac = 0;     // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC); 0 = by kernel:
                          // 50 for the compact-box kernels (scene 8 1080p -1.1%, 4K -1.6% against 56), 56 else
                          // (scene 6 +1.4% at 52; profiles/r03_sm_frac_knobs.log)
+    bool leaf_prefetch = true;   // leaf records prefetched before the type blocks when all are in LDS (option)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
     bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
     bool sph_lds = true;   // sphere records' first two float4 in LDS when they fit (env RT_SPH_LDS=0 disables; A/B)
@@ -1696,6 +1697,10 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             }
         }
         a.lds_end_f4 = (int)at;
+        // the leaf stage's record prefetch reads 3 float4 at any of these tables' offsets: every
+        // table it can index is staged (and a sphere's 3rd float4 stays inside the staged region)
+        a.leaf_pf = (c->leaf_prefetch && a.sph_lds >= 0 && a.box_cmp_lds >= 0 &&
+                     (n_med == 0 || a.media_lds >= 0) && a.box_cmp_lds > a.sph_lds) ? 1 : 0;
     }
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
@@ -2185,6 +2190,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_PERLIN_PACKED: c->perlin_pk = v != 0; break;
         case RT_OPTION_SPARSE_STAGE: c->sparse_stage = v != 0; break;
         case RT_OPTION_SPHERE_PAIRS: c->sphere_pairs = v != 0; break;
+        case RT_OPTION_LEAF_PREFETCH: c->leaf_prefetch = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2219,6 +2225,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_PERLIN_PACKED: *v = c->perlin_pk; break;
         case RT_OPTION_SPARSE_STAGE: *v = c->sparse_stage; break;
         case RT_OPTION_SPHERE_PAIRS: *v = c->sphere_pairs; break;
+        case RT_OPTION_LEAF_PREFETCH: *v = c->leaf_prefetch; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

@@ -120,6 +120,8 @@ struct rt_kernel_args {
     int sm_frac;                 // or this many 64ths of the lanes with a walk (or none runs)
     int walk_frac;               // render_sm: a round's node walk stops once this many 64ths of its lanes
                                  // hold a leaf or ended (64: all of them)
+    int leaf_pf;                 // BOXC kernels: the leaf stage prefetches each slot's record (spheres, boxes
+                                 // and media all staged in LDS; rt_kernel.hip leaf_prims_t)
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)
@@ -180,7 +182,7 @@ struct rt_kernel_args {
 
 // What rt_launch_render launched (rt_debug_last_launch)
 enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
-       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_N = 16 };
+       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_LEAF_PF, RT_LI_N = 16 };
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)

@@ -445,6 +445,27 @@ __device__ __forceinline__ bool medium_tail(float neg_inv_density, float t1, flo
     return true;
 }
 
+// medium_test on the medium's LDS record already loaded (R0 = boundary idx, type, -1/density, phase;
+// R1, R2 = its sphere boundary's A, B when the boundary is a sphere): the same operations.
+template <bool FD = false>
+__device__ __forceinline__ bool medium_test_rec(const KP& P, float4 R0, float4 R1, float4 R2, v3 o, v3 d, float a,
+                                                float time, float tmin, float tmax, float& rf, float px, float py,
+                                                float& t) {
+    float t1, t2;
+    rt_medium m;
+    m.boundary_idx = __float_as_int(R0.x);
+    m.boundary_type = __float_as_int(R0.y);
+    m.neg_inv_density = R0.z;
+    m.phase_material = __float_as_int(R0.w);
+    m.texture_id = 0;
+    if (m.boundary_type == RT_MODEL_SPHERE) {
+        if (!sphere_bounds(R1, R2, o, d, a, time, t1, t2, FD)) return false;
+    } else if (!medium_bounds(P, m, o, d, a, time, t1, t2)) {
+        return false;
+    }
+    return medium_tail(m.neg_inv_density, t1, t2, a, tmin, tmax, rf, px, py, t);
+}
+
 // hitting.glsl:162-193 — returns the hit distance t.
 template <bool FD = false>
 __device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin,
@@ -601,9 +622,28 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
         float t = 0.0f, al = 0.0f, be = 0.0f;
         int face = 0;
         bool hit = false;
+        // Record prefetch (BOXC kernels whose sphere, box and medium records are all in LDS,
+        // P.leaf_pf): the slot's record -- a sphere's (A, B), a box's compact record, a medium's
+        // record and sphere boundary, each 3 float4 from its table's offset -- is loaded once for
+        // every lane before the type blocks, so the blocks do not each wait on their own LDS
+        // round trip.  (A sphere's third float4 is its successor's A, or the next table's first:
+        // in LDS, unused.)  The same values reach the same tests.
+        const bool pf = BOXC && P.leaf_pf;   // wave-uniform
+        float4 q0, q1, q2;
+        if (pf) {
+            const int off = ty == RT_MODEL_SPHERE ? P.sph_lds + 2 * ix
+                          : ty == RT_MODEL_BOX ? P.box_cmp_lds + RT_BOXC_F4 * ix
+                          : ty == RT_MODEL_CONSTANT_MEDIUM ? P.media_lds + 3 * ix : 0;
+            const float4* r = rt_dyn_lds + off;
+            q0 = r[0];
+            q1 = r[1];
+            q2 = r[2];
+        }
         unsigned long long c0 = STATS ? clock64() : 0;
         if (ty == RT_MODEL_SPHERE) {
-            if (P.sph_lds >= 0) {   // the record's intersection half from LDS (render_persistent)
+            if (pf) {
+                hit = sphere_t_ab(q0, q1, time, o, d, a, tmin, tmax, t, fd, fd ? rcp_nr(a) : 0.0f);
+            } else if (P.sph_lds >= 0) {   // the record's intersection half from LDS (render_persistent)
                 const float4* r = rt_dyn_lds + P.sph_lds + 2 * ix;
                 hit = sphere_t_ab(r[0], r[1], time, o, d, a, tmin, tmax, t, fd, fd ? rcp_nr(a) : 0.0f);
             } else {
@@ -624,7 +664,11 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             // non-finite origin or direction, in the reference's form or the compact one (its
             // plane t or its alpha / beta is then inf or NaN), so BOXC needs no finiteness check.
             float4 r0, r1, r2;
-            if (P.box_cmp_lds >= 0) {
+            if (pf) {
+                r0 = q0;
+                r1 = q1;
+                r2 = q2;
+            } else if (P.box_cmp_lds >= 0) {
                 const float4* cr = rt_dyn_lds + P.box_cmp_lds + RT_BOXC_F4 * ix;
                 r0 = cr[0];
                 r1 = cr[1];
@@ -652,7 +696,8 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
-            hit = medium_test<FD>(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
+            hit = pf ? medium_test_rec<FD>(P, q0, q1, q2, o, d, a, time, tmin, tmax, rf, px, py, t)
+                     : medium_test<FD>(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
             if (STATS) st_add(st, ST_MED_CYC, clock64() - c0);
         }
         if (hit) {
@@ -2467,6 +2512,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         return -1;
     if (shape == LINK_TL && (a.block != 1024 || !pool)) return -1;
     if (pool && !a.samples && !a.wbuf) return -1;   // pooled ordered / one-chunk units need the per-wave slots
+    // the leaf record prefetch reads only tables that are staged (the A/B shapes above may drop them)
+    a.leaf_pf = (a.leaf_pf && a.box_all_cmp && a.sph_lds >= 0 && a.box_cmp_lds > a.sph_lds &&
+                 (a.n_media == 0 || a.media_lds >= 0)) ? 1 : 0;
     // the one-pixel-per-lane kernels (A/B) keep the lanes' running means in LDS after what is staged
     a.acc_lds = (int)(staged / 16);
     const size_t lds = staged + (pool ? 0 : RT_LDS_ACC_BYTES);
@@ -2483,6 +2531,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         info[RT_LI_SPINE] = pool ? a.spine_len : 0;
         info[RT_LI_SPARSE] = a.samples && a.sflags ? 1 : 0;
         info[RT_LI_SPAIR] = (pool && shape == LINK_LDS && a.sph_pairs && !a.box_all_cmp && a.sph_lds >= 0) ? 1 : 0;
+        info[RT_LI_LEAF_PF] = (pool && (shape == LINK_LDS || shape == LINK_TL)) ? a.leaf_pf : 0;
     }
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.

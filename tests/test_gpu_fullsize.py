@@ -155,7 +155,7 @@ def test_lds_record_copies_change_no_bit_1080p(gpu, knob, sid):
 WALK_OPTIONS = [
     ("sm_frac", {"sm_frac": 8}), ("sm_frac", {"sm_frac": 64}), ("sm_batch", {"sm_batch": 16}),
     ("walk_frac", {"walk_frac": 16}), ("walk_frac", {"walk_frac": 64}),
-    ("sphere_pairs", {"sphere_pairs": 0}), ("spine", {"spine": 0}),
+    ("sphere_pairs", {"sphere_pairs": 0}), ("spine", {"spine": 0}), ("leaf_prefetch", {"leaf_prefetch": 0}),
     ("two_level", {"lds_node_cap": 16384}), ("two_level_leaf_global", {"lds_node_cap": 16384, "tl_leaf_lds": 0}),
 ]
 

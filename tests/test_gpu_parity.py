@@ -48,6 +48,25 @@ def test_perlin_table_forms_match_oracle(gpu, scene_id, packed):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
+@pytest.mark.parametrize("scene_id,want", [(8, 1), (0, 0), (6, 0), (7, 0)])
+def test_leaf_record_prefetch_matches_oracle(gpu, scene_id, want):
+    """The compact-box kernels' leaf record prefetch (rt_kernel.hip leaf_prims_t, option
+    leaf_prefetch): scene 8 (every box canonical; spheres, boxes and media staged in LDS) takes
+    it, the others not (asserted); on and off, bit for bit against the oracle."""
+    s = rtamd.Scene(scene_id, 48, 27, seed=1)
+    ref = oracle_image(s, 6, max_depth=5)
+    for opts, w in (({}, want), ({"leaf_prefetch": 0}, 0)):
+        ctx = rtamd.RenderContext(options=opts)
+        ctx.upload_scene(s)
+        ctx.set_params(max_depth=5, spp=4096)
+        ctx.resize(48, 27)
+        ctx.render(1, rtamd.frame_rand_factors(1, 0, 6))
+        out, info = ctx.read_image(), ctx.last_launch()
+        ctx.close()
+        assert info["leaf_prefetch"] == w, (opts, info)
+        assert bit_equal(out, ref), f"{opts}: {mismatch_report(out, ref)}"
+
+
 @pytest.mark.parametrize("scene_id,pairs", [(0, 1), (1, 1), (9, 1), (8, 0), (6, 0)])
 def test_sphere_pair_kernel_matches_oracle(gpu, scene_id, pairs):
     """Scenes whose leaves are mostly two spheres take the kernels that test both at once
