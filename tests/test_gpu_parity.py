@@ -58,7 +58,7 @@ def test_leaf_record_prefetch_matches_oracle(gpu, scene_id, want):
     for opts, w in (({}, want), ({"leaf_prefetch": 0}, 0)):
         ctx = rtamd.RenderContext(options=opts)
         ctx.upload_scene(s)
-        ctx.set_params(max_depth=5, spp=4096)
+        ctx.set_params(max_depth=5, spp=6)   # the oracle_image default: spp = frames
         ctx.resize(48, 27)
         ctx.render(1, rtamd.frame_rand_factors(1, 0, 6))
         out, info = ctx.read_image(), ctx.last_launch()
