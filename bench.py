@@ -326,6 +326,8 @@ def main():
     torch.cuda.synchronize()
     tg = time.perf_counter()
     try:
+        if os.environ.get("RT_BENCH_GATHER") == "torch":   # escape hatch: the torch gather only
+            raise RuntimeError("RT_BENCH_GATHER=torch")
         full = rdist.native_gather(ctx, rank, world)
         gather_path = "rt_gather_image (RCCL send/recv + device de-interleave)" if world > 1 \
             else "rt_read_image (world 1)"

@@ -62,10 +62,21 @@ def native_gather(ctx, rank, world):
     de-interleave kernel there): rank 0 makes the communicator id, torch.distributed
     hands it to the other ranks (the only use of torch.distributed here).  Returns the
     [H, W, 4] image on rank 0, None elsewhere."""
-    from .render import comm_unique_id
+    from . import render
     if world == 1:
         return ctx.read_image()
-    box = [comm_unique_id() if rank == 0 else None]
+    # rank 0 always takes part in the broadcast, id or not, so a failure to make the id (RCCL
+    # not loadable) raises on every rank instead of leaving the others waiting for it
+    uid, err = None, None
+    if rank == 0:
+        try:
+            uid = render.comm_unique_id()
+        except Exception as e:  # noqa: BLE001 -- reported on every rank below
+            err = repr(e)
+    box = [(uid, err)]
     dist.broadcast_object_list(box, src=0)
-    ctx.comm_init(box[0], rank, world)
+    uid, err = box[0]
+    if uid is None:
+        raise RuntimeError(f"rank 0 could not make an RCCL communicator id: {err}")
+    ctx.comm_init(uid, rank, world)
     return ctx.gather_image()

@@ -100,7 +100,7 @@ def test_native_gather_world1_is_read_image():
     assert out is img and c.calls == ["read_image"]
 
 
-def _native_worker(rank, world, port, q):
+def _native_worker(rank, world, port, q, fail=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         rdist.init_from_env(backend="gloo")
@@ -108,11 +108,16 @@ def _native_worker(rank, world, port, q):
 
         def fake_uid():
             assert rank == 0, "only rank 0 makes the communicator id"
+            if fail:
+                raise OSError("librccl.so.1: cannot open shared object file")
             return bytes(range(7, 7 + 128))
         R.comm_unique_id = fake_uid
         c = _FakeCtx(rank, np.full((3, 2, 4), 5.0, np.float32) if rank == 0 else None)
-        out = rdist.native_gather(c, rank, world)
-        q.put((rank, c.uid, c.calls, None if out is None else out.shape))
+        try:
+            out = rdist.native_gather(c, rank, world)
+            q.put((rank, c.uid, c.calls, None if out is None else out.shape))
+        except RuntimeError as e:
+            q.put((rank, "raised", c.calls, str(e)))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # report, never hang the parent
@@ -145,6 +150,29 @@ def test_native_gather_hands_rank0_id_to_every_rank():
         _, got, calls, shape = by_rank[r]
         assert got == uid and calls == [("comm_init", r, world), "gather_image"], (r, calls)
         assert shape == ((3, 2, 4) if r == 0 else None)
+
+
+def test_native_gather_id_failure_raises_on_every_rank():
+    """If rank 0 cannot make the RCCL id, every rank raises (none waits for a broadcast that
+    never comes); bench.py then falls back to the torch gather on all ranks."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_worker, args=(r, world, port, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not q.empty():
+        msgs.append(q.get())
+    assert sorted(m[0] for m in msgs) == [0, 1], msgs
+    for m in msgs:
+        assert m[1] == "raised" and m[2] == [] and "cannot open" in m[3], m
 
 
 def test_bench_cpu_threads_follow_the_quota():
