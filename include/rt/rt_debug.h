@@ -35,9 +35,6 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
  * (types | next address << 8, prims) as uint2.  *n_f4 = its float4 count, 0 when
  * there is no BVH. */
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4);
-/* The same with only the first n_bfs nodes placed breadth-first and each remaining subtree
- * in threaded (pre-order, right child first) order after them: the two-level walk's layout. */
-int rt_debug_link_nodes_bfs(const void* bvh, size_t nbytes, int n_bfs, void* out, size_t out_cap, int* n_f4);
 
 /* Host-only: the packed Perlin table rt_upload_texture keeps beside an R32F 6 x 256 texture
  * whose perm columns (3..5) hold whole numbers 0..255: 256 float4 (ranvec x, y, z; the three
@@ -112,8 +109,6 @@ enum {
     RT_OPTION_LEAF_PREFETCH = 20,       /* compact-box kernels: each leaf slot's record loaded
                                            before the prim-type blocks when spheres, boxes
                                            and media are all staged in LDS (1)              */
-    RT_OPTION_TL_DFS = 21,              /* two-level walk: nodes below the LDS prefix laid
-                                           out subtree by subtree (1)                       */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

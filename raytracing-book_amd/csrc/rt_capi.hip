@@ -168,8 +168,6 @@ struct rt_ctx {
     int sm_frac = 0;     // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC); 0 = by kernel:
                          // 50 for the compact-box kernels (scene 8 1080p -1.1%, 4K -1.6% against 56), 56 else
                          // (scene 6 +1.4% at 52; profiles/r03_sm_frac_knobs.log)
-    bool tl_dfs = true;          // two-level walk: the nodes below the LDS prefix in subtree order (option)
-    size_t links_bfs = (size_t)-1;   // breadth-first prefix of c->links' layout (all of it: -1)
     bool leaf_prefetch = true;   // leaf records prefetched before the type blocks when all are in LDS (option)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
     bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
@@ -368,15 +366,7 @@ bool boxes_nest(const std::vector<rt_dnode>& dn) {
 // sequence (tests/test_link_nodes.py), and the top levels every ray walks sit at the
 // lowest addresses, the part a two-level launch stages in LDS.  Empty when there is
 // no BVH or it has more nodes than 16-bit indices address.
-//
-// n_bfs < n (the two-level walk, rt_render): only the first n_bfs nodes of that order -- the
-// prefix a two-level launch stages in LDS -- are placed breadth-first; each subtree still
-// waiting in the breadth-first queue then follows whole, in the threaded array's own order
-// (pre-order, right child first: a subtree is the contiguous range [r, skip(r))).  Below the LDS
-// prefix a walk's next node is then mostly the next 32 bytes -- an inner node's hit successor is
-// its right child, a right leaf's miss successor its left sibling -- so the global-memory steps
-// hit the cache line the previous step brought in.  The same successors, the same sequence.
-std::vector<float4> build_links(const std::vector<rt_dnode>& dn, size_t n_bfs = (size_t)-1) {
+std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
     std::vector<float4> out;
     const size_t n = dn.size();
     if (n == 0 || n > RT_LINK_MAX_NODES) return out;
@@ -384,8 +374,7 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, size_t n_bfs = 
     std::vector<uint32_t> pos(n, 0xFFFFFFFFu), order;
     order.reserve(n);
     order.push_back(0);
-    size_t h = 0;
-    for (; h < order.size() && h < n_bfs; h++) {
+    for (size_t h = 0; h < order.size(); h++) {
         const uint32_t k = order[h];
         if (pos[k] != 0xFFFFFFFFu || order.size() > n) return std::vector<float4>();
         pos[k] = (uint32_t)h;
@@ -394,20 +383,6 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, size_t n_bfs = 
         if (k + 1 >= n || l == RT_NODE_END || l >= n) return std::vector<float4>();
         order.push_back(k + 1);
         order.push_back(l);
-    }
-    if (h < order.size()) {   // the queued subtrees, each whole in threaded order
-        std::vector<uint32_t> roots(order.begin() + (long)h, order.end());
-        order.resize(h);
-        for (const uint32_t r : roots) {
-            const uint32_t sk = dn[r].meta & 0xFFFFu;
-            const size_t end = sk == RT_NODE_END ? n : (size_t)sk;
-            if (end <= r || end > n) return std::vector<float4>();
-            for (size_t k = r; k < end; k++) {
-                if (pos[k] != 0xFFFFFFFFu) return std::vector<float4>();
-                pos[k] = (uint32_t)order.size();
-                order.push_back((uint32_t)k);
-            }
-        }
     }
     if (order.size() != n) return out;
     size_t nl = 0;
@@ -977,7 +952,6 @@ int validate(rt_ctx* c) {
     c->fast = build_fast(c->dnodes, ns, (const rt_quad*)QB.data(), nq, (const rt_box*)BB.data(), nb);
     c->fast.ok = c->fast.ok && c->spec_ok && !c->uv_always;
     c->links = build_links(c->dnodes);
-    c->links_bfs = (size_t)-1;
     c->pair_leaves = -1;
     c->fast_gen++;
     c->validated = true;
@@ -1629,6 +1603,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
     a.debug_flags = c->debug_flags;
     a.n_lnode_f4 = (int)c->links.size();
+    plan_spine(c->links, c->n_dnodes, c->cam, c->spine, a);
     // LDS plan of the link-format shapes (rt_kernel.hip rt_launch_render): from address 0 the
     // nodes, then the leaf records, the Perlin table (6 x 256 R32F), the media records with
     // their sphere boundaries, the spheres' intersection halves (A, B) and the canonical
@@ -1722,21 +1697,11 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             }
         }
         a.lds_end_f4 = (int)at;
-        // the node layout for this plan (build_links): breadth-first throughout, or -- two-level
-        // walk -- breadth-first for the LDS prefix and subtree order below it
-        const size_t want_bfs = (tl && c->tl_dfs && a.lds_node_f4 > 0) ? (size_t)a.lds_node_f4 / 2 : (size_t)-1;
-        if (a.n_lnode_f4 > 0 && want_bfs != c->links_bfs) {
-            c->links = build_links(c->dnodes, want_bfs);
-            c->links_bfs = want_bfs;
-            c->fast_gen++;   // re-upload (rt_render below)
-        }
         // the leaf stage's record prefetch reads 3 float4 at any of these tables' offsets: every
         // table it can index is staged (and a sphere's 3rd float4 stays inside the staged region)
         a.leaf_pf = (c->leaf_prefetch && a.sph_lds >= 0 && a.box_cmp_lds >= 0 &&
                      (n_med == 0 || a.media_lds >= 0) && a.box_cmp_lds > a.sph_lds) ? 1 : 0;
     }
-    // spine entry over the layout this launch uses (its start is an address in it)
-    plan_spine(c->links, c->n_dnodes, c->cam, c->spine, a);
     a.cam = c->cam;
     std::memcpy(a.background, c->background, 12);
     a.max_depth = c->max_depth;
@@ -2103,21 +2068,6 @@ int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_ca
     return RT_OK;
 }
 
-int rt_debug_link_nodes_bfs(const void* bvh, size_t nbytes, int n_bfs, void* out, size_t out_cap, int* n_f4) {
-    if (!bvh || !n_f4 || nbytes % sizeof(rt_bvh_node) || n_bfs < 0) return RT_ERR_INVALID_ARG;
-    std::vector<rt_dnode> dn;
-    rt_ctx tmp;
-    int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
-    if (r) return r;
-    const std::vector<float4> L = build_links(dn, (size_t)n_bfs);
-    *n_f4 = (int)L.size();
-    if (out) {
-        if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
-        std::memcpy(out, L.data(), L.size() * sizeof(float4));
-    }
-    return RT_OK;
-}
-
 int rt_debug_perlin_pack(const float* texels, int w, int h, void* out, size_t out_cap) {
     if (!texels || w <= 0 || h <= 0) return RT_ERR_INVALID_ARG;
     std::vector<float4> pk;
@@ -2241,7 +2191,6 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SPARSE_STAGE: c->sparse_stage = v != 0; break;
         case RT_OPTION_SPHERE_PAIRS: c->sphere_pairs = v != 0; break;
         case RT_OPTION_LEAF_PREFETCH: c->leaf_prefetch = v != 0; break;
-        case RT_OPTION_TL_DFS: c->tl_dfs = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2277,7 +2226,6 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_SPARSE_STAGE: *v = c->sparse_stage; break;
         case RT_OPTION_SPHERE_PAIRS: *v = c->sphere_pairs; break;
         case RT_OPTION_LEAF_PREFETCH: *v = c->leaf_prefetch; break;
-        case RT_OPTION_TL_DFS: *v = c->tl_dfs; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

@@ -89,15 +89,13 @@ def test_scenes_walks_skip_their_spine(gpu, sid, spine):
 @pytest.mark.parametrize("cap", [4096, 32768, 65536])
 def test_two_level_walk_forced(gpu, cap, tll):
     """The ~4000-node cloud, which fits LDS, with only `cap` bytes of its nodes staged and its
-    leaf records in LDS (tll 1) or global memory, and the nodes below the LDS prefix in subtree
-    order (tl_dfs, default) or breadth-first: the same bits as the oracle whatever the split
-    between LDS and global nodes and whatever their layout."""
+    leaf records in LDS (tll 1) or global memory: the same bits as the oracle whatever the
+    split between LDS and global nodes."""
     case = next(c for c in CASES if c.name == "bvh_4k_lds")
     ref = oracle(case)
-    for dfs in (1, 0):
-        out, info = render(case, {"lds_node_cap": cap, "tl_leaf_lds": tll, "tl_dfs": dfs})
-        assert info["shape_name"] == "link-two-level" and info["lds_nodes"] == cap // 32, info
-        assert bit_equal(out, ref), f"tl_dfs {dfs}: " + mismatch_report(out, ref)
+    out, info = render(case, {"lds_node_cap": cap, "tl_leaf_lds": tll})
+    assert info["shape_name"] == "link-two-level" and info["lds_nodes"] == cap // 32, info
+    assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
 def test_watchdog_fault_is_reported(gpu):

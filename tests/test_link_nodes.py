@@ -23,22 +23,13 @@ from test_fast_tables import END, is_leaf, threaded
 LEAF, LEND, NEXT_END = 0x80000000, 0xFFFFFFFF, 0xFFFFFF
 
 
-def links_of(bvh_bytes, n_bfs=None):
-    """rt_debug_link_nodes (breadth-first throughout), or with n_bfs the two-level walk's layout
-    (rt_debug_link_nodes_bfs: the first n_bfs nodes breadth-first, then whole subtrees)."""
+def links_of(bvh_bytes):
     L = rtamd.amd()
     bvh = ctypes.create_string_buffer(bvh_bytes, len(bvh_bytes))
     n = ctypes.c_int()
-    if n_bfs is None:
-        assert L.rt_debug_link_nodes(bvh, len(bvh_bytes), None, 0, ctypes.byref(n)) == 0
-    else:
-        assert L.rt_debug_link_nodes_bfs(bvh, len(bvh_bytes), n_bfs, None, 0, ctypes.byref(n)) == 0
+    assert L.rt_debug_link_nodes(bvh, len(bvh_bytes), None, 0, ctypes.byref(n)) == 0
     out = np.zeros((max(n.value, 1), 4), np.float32)
-    if n_bfs is None:
-        assert L.rt_debug_link_nodes(bvh, len(bvh_bytes), out.ctypes.data, out.nbytes, ctypes.byref(n)) == 0
-    else:
-        assert L.rt_debug_link_nodes_bfs(bvh, len(bvh_bytes), n_bfs, out.ctypes.data, out.nbytes,
-                                         ctypes.byref(n)) == 0
+    assert L.rt_debug_link_nodes(bvh, len(bvh_bytes), out.ctypes.data, out.nbytes, ctypes.byref(n)) == 0
     return out[:n.value]
 
 
@@ -52,21 +43,15 @@ def threaded_of(bvh_bytes):
     return out
 
 
-def bfs_order(tn, n_bfs=None):
+def bfs_order(tn):
     """Breadth-first order of the threaded nodes: an inner node k's children are its
-    right child k + 1 and its left child skip(k + 1).  With n_bfs, only the first n_bfs
-    nodes; each subtree still queued then follows whole in threaded order [r, skip(r))."""
+    right child k + 1 and its left child skip(k + 1)."""
     order, h = [0], 0
-    lim = len(tn) if n_bfs is None else n_bfs
-    while h < len(order) and h < lim:
+    while h < len(order):
         k = order[h]
         h += 1
         if not is_leaf(tn[k]):
             order += [k + 1, int(tn[k + 1]["meta"]) & 0xFFFF]
-    roots, order = order[h:], order[:h]
-    for r in roots:
-        sk = int(tn[r]["meta"]) & 0xFFFF
-        order += list(range(r, len(tn) if sk == END else sk))
     return order
 
 
@@ -106,9 +91,9 @@ def walk_links(ln, n, hits, node_of_slot):
     return seen, tested
 
 
-def check_layout(tn, ln, n_bfs=None):
+def check_layout(tn, ln):
     n = len(tn)
-    order = bfs_order(tn, n_bfs)
+    order = bfs_order(tn)
     assert sorted(order) == list(range(n))
     pos = np.empty(n, np.int64)
     pos[order] = np.arange(n)
@@ -177,36 +162,3 @@ def test_link_format_reaches_the_16_bit_node_limit(n_leaves):
         for p in (0.5, 0.9, 1.0):
             hits = rng.random(len(tn)) < p
             assert walk_links(ln, len(tn), hits, order) == walk_threaded(tn, hits)
-
-
-@pytest.mark.parametrize("n_bfs", [0, 1, 2, 7, 100, 1023])
-@pytest.mark.parametrize("src", ["scene8", "heap2048", "cloud"])
-def test_two_level_layout_replays_threaded_walk(src, n_bfs):
-    """The two-level walk's layout (rt_capi.hip build_links with an LDS prefix): the first n_bfs
-    nodes breadth-first, every subtree below them whole in threaded order.  Same boxes and
-    successors, the same node sequence under any hit pattern; below the prefix an inner node's
-    hit successor is the next node (its right child)."""
-    if src == "scene8":
-        b = rtamd.Scene(8, 64, 36, seed=1).buffers[1]
-    elif src == "heap2048":
-        b = heap_bvh(2048)
-    else:
-        import adversarial
-        b = adversarial.sphere_cloud(1500, 4).buffers[1]
-    b = bytes(b)
-    tn = threaded_of(b)
-    ln = links_of(b, n_bfs)
-    order = check_layout(tn, ln, n_bfs)
-    n = len(tn)
-    pos = np.empty(n, np.int64)
-    pos[order] = np.arange(n)
-    for k in range(n):
-        if pos[k] >= n_bfs and not is_leaf(tn[k]):
-            assert pos[k + 1] == pos[k] + 1   # hit successor adjacent below the prefix
-    rng = np.random.default_rng(n_bfs + len(src))
-    for p in (0.3, 0.8, 1.0):
-        for _ in range(5):
-            hits = rng.random(n) < p
-            assert walk_links(ln, n, hits, order) == walk_threaded(tn, hits)
-    if n_bfs >= n:
-        assert np.array_equal(ln.view(np.uint32), links_of(b).view(np.uint32))

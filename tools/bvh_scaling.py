@@ -45,14 +45,13 @@ def main():
         sc = adversarial.sphere_cloud(n, seed, W=W, H=H)
         caps = [0] if n != 4000 else [0, 98304, 65536, 32768, 8192]
         for cap in caps:
-            # the two-level walk with the nodes below its LDS prefix in subtree order (default,
-            # option tl_dfs) and breadth-first (round 3's layout)
-            for dfs in ((1, 0) if (cap or n == 9000) else (1,)):
+            # the two-level walk with its leaf records in LDS (default) and in global memory
+            for tll in ((1, 0) if (cap or n == 9000) else (1,)):
                 opts = {"lds_node_cap": cap} if cap else {}
-                if not dfs:
-                    opts["tl_dfs"] = 0
+                if not tll:
+                    opts["tl_leaf_lds"] = 0
                 rate, ms, info = timed(sc, opts)
-                row = {"spheres": n, "bvh_nodes": sc.info["n_bvh_nodes"], "lds_node_cap": cap, "tl_dfs": dfs,
+                row = {"spheres": n, "bvh_nodes": sc.info["n_bvh_nodes"], "lds_node_cap": cap, "tl_leaf_lds": tll,
                        "Msamples_s": round(rate, 1), "ms_per_launch": round(ms, 3), "shape": info["shape_name"],
                        "block": info["block"], "lds_nodes": info["lds_nodes"], "lds_bytes": info["lds_bytes"]}
                 rows.append(row)
@@ -60,7 +59,7 @@ def main():
     base = next(r for r in rows if r["spheres"] == 4000 and r["lds_node_cap"] == 0)["Msamples_s"]
     for r in rows:
         if r["spheres"] == 4000:
-            print(json.dumps({"spheres": 4000, "lds_node_cap": r["lds_node_cap"], "tl_dfs": r["tl_dfs"],
+            print(json.dumps({"spheres": 4000, "lds_node_cap": r["lds_node_cap"], "tl_leaf_lds": r["tl_leaf_lds"],
                               "cost_vs_all_in_lds": round(base / r["Msamples_s"], 3)}), flush=True)
 
 
