@@ -115,32 +115,41 @@ RT_HD v3 g_mat3_mul(v3 c0, v3 c1, v3 c2, v3 v) {
 }
 
 /* ------------------------------------------------------ transcendentals */
-/* sin/cos: Cody–Waite reduction by pi/2 in three fma steps (exact to ~2^-70
- * for |x| < 2^20), then minimax polynomials on [-pi/4, pi/4]. */
-RT_HD void g_sincos(float x, float* s_out, float* c_out) {
-    float j = rintf(x * 0.636619746685028076171875f);
-    float r = fmaf(j, -1.57079637050628662109375f, x);
-    r = fmaf(j, 4.37113882867379300296306610107421875e-8f, r);
-    r = fmaf(j, 1.71512451000588190000000000e-15f, r);
-    float z = r * r;
-    float sp = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
-    float cp = fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
-                              4.166664568298827e-2f), z, -0.5f), z, 1.0f);
-    /* quadrant q = rt_f2i(j) & 3 without branches: NaN -> -2^31 (fmaxf drops it) and
-     * j <= -2^31 give INT_MIN (q 0, as rt_f2i's 0 / INT_MIN), j >= 2147483520 gives
-     * rt_f2i's INT_MAX (q 3), the rest converts in range. */
-    const float jc = fminf(fmaxf(j, -2147483648.0f), 2147483520.0f);
-    int q = (int)jc & 3;
-    q = (j >= 2147483520.0f) ? 3 : q;
-    /* q 0..3: (s, c) = (sp, cp), (cp, -sp), (-sp, -cp), (-cp, sp) */
-    float s = (q & 1) ? cp : sp;
-    float c = (q & 1) ? -sp : cp;
-    s = (q & 2) ? -s : s;
-    c = (q & 2) ? -c : c;
-    *s_out = s; *c_out = c;
+/* sin/cos (round 4): reduction by pi -- x = j*pi + r, |r| <= pi/2, Cody-Waite in three fma
+ * steps -- then one odd degree-9 polynomial for sin(r) (coefficients tuned in float32: within
+ * 1.51 ulp of sin on [-pi/2, pi/2]) and the sign of (-1)^j.  cos(x) = (-1)^(j+1) sin(r) with
+ * x = (j + 1/2) pi + r.  Every GLSL sin() / cos() of the reference is one of these (rand()'s
+ * hash, the cosine and sphere-light directions, the marble texture); round 3 reduced by pi/2
+ * and evaluated both a sine and a cosine polynomial with a quadrant select for every call,
+ * ~25 operations against ~15 here.  The parity of j is taken in float (j/2 against its floor):
+ * exact below 2^24, and every float from 2^24 up is an even integer; NaN and +-inf give NaN.
+ * Deterministic and branch-free on both sides; accurate to ~1e-7 absolute for |x| < 2^20. */
+RT_HD float rt_sin_poly(float r) {
+    const float z = r * r;
+    const float p = fmaf(fmaf(fmaf(2.6000548132287804e-06f, z, -1.9806638010777533e-04f), z,
+                              8.333016186952591e-03f), z, -1.6666656732559204e-01f);
+    return fmaf(p, z * r, r);
 }
-RT_HD float g_sin(float x) { float s, c; g_sincos(x, &s, &c); return s; }
-RT_HD float g_cos(float x) { float s, c; g_sincos(x, &s, &c); return c; }
+RT_HD float rt_neg_if_odd(float s, float j) {
+    const float h = j * 0.5f;
+    return (h != floorf(h)) ? -s : s;
+}
+RT_HD float g_sin(float x) {
+    const float j = rintf(x * 0x1.45f306p-2f);                  /* 1/pi */
+    float r = fmaf(j, -0x1.921fb6p+1f, x);                       /* pi = A + B + C */
+    r = fmaf(j, 0x1.777a5cp-24f, r);
+    r = fmaf(j, 0x1.ee59dap-49f, r);
+    return rt_neg_if_odd(rt_sin_poly(r), j);
+}
+RT_HD float g_cos(float x) {
+    const float j = rintf(fmaf(x, 0x1.45f306p-2f, -0.5f));      /* x = (j + 1/2) pi + r */
+    const float jh = j + 0.5f;
+    float r = fmaf(jh, -0x1.921fb6p+1f, x);
+    r = fmaf(jh, 0x1.777a5cp-24f, r);
+    r = fmaf(jh, 0x1.ee59dap-49f, r);
+    return rt_neg_if_odd(-rt_sin_poly(r), j);
+}
+RT_HD void g_sincos(float x, float* s_out, float* c_out) { *s_out = g_sin(x); *c_out = g_cos(x); }
 
 /* natural log: exponent/mantissa split (m in [sqrt(1/2), sqrt(2))), degree-9
  * polynomial for log(1+f), Cody–Waite ln2 split. */
