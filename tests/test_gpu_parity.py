@@ -116,8 +116,8 @@ def test_builtins_bit_exact_on_device(gpu):
     for name, lo, hi in [("sin", -3e5, 3e5), ("cos", -100, 100), ("log", 0, 1), ("acos", -1, 1), ("atan2", -5, 5),
                          ("fract", -1e4, 1e4), ("sqrt", 0, 1e6)]:
         x = rng.uniform(lo, hi, 20000).astype(np.float32)
-        # the branch-free special cases (rt_glsl.h g_log, g_sincos's quadrant): NaN, signed
-        # zeros and infinities, negatives, subnormals, quadrants past int range
+        # the branch-free special cases (rt_glsl.h g_log, g_sin / g_cos's parity of j): NaN,
+        # signed zeros and infinities, negatives, subnormals, arguments past 2^24
         x[:SPECIALS.size] = SPECIALS
         y = rng.uniform(-5, 5, 20000).astype(np.float32)
         ref = pyoracle.eval_builtin(name, x, y)

@@ -78,9 +78,9 @@ def test_builtin_accuracy(name, fn, lo, hi, max_ulp):
 
 
 def test_builtin_special_cases():
-    """g_log's and g_sincos's special inputs (both branch-free in rt_glsl.h): NaN and x < 0 give
-    NaN, +-0 gives -inf, +inf gives +inf, subnormals are scaled into range; sin / cos of NaN and
-    of +-inf are NaN."""
+    """g_log's and g_sin / g_cos's special inputs (all branch-free in rt_glsl.h): NaN and x < 0
+    give NaN, +-0 gives -inf, +inf gives +inf, subnormals are scaled into range; sin / cos of NaN
+    and of +-inf are NaN."""
     x = np.array([np.nan, -1.0, -1e-30, 0.0, -0.0, np.inf], np.float32)
     got = pyoracle.eval_builtin("log", x)
     assert np.isnan(got[:3]).all() and (got[3:5] == -np.inf).all() and got[5] == np.inf
@@ -88,8 +88,8 @@ def test_builtin_special_cases():
     assert (_ulp_err(pyoracle.eval_builtin("log", sub), np.log(sub.astype(np.float64))) <= 2.0).all()
     for name in ("sin", "cos"):
         assert np.isnan(pyoracle.eval_builtin(name, np.array([np.nan, np.inf, -np.inf], np.float32))).all()
-        # past |x| ~ 2^20 the reduction is not accurate (defined, deterministic; the quadrant
-        # follows rt_f2i's saturation: tools/glsl_equiv.sh compares it with the branchy form)
+        # past |x| ~ 2^20 the reduction is not accurate (defined, deterministic: from 2^24 every
+        # j is an even integer, so the sign is +)
         big = np.array([3.3732712e9, 3.3732714e9, -3.4028235e38, 1e10], np.float32)
         assert np.array_equal(pyoracle.eval_builtin(name, big).view(np.uint32),
                               pyoracle.eval_builtin(name, big).view(np.uint32))
