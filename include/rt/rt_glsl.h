@@ -10,7 +10,7 @@
  * rint and exact integer/bit operations, so the same source compiled by g++
  * (oracle, x86-64 SSE) and by hipcc (gfx950 kernel) produces identical bits as
  * long as both are built with -ffp-contract=off and without fast-math
- * (correctly-rounded f32 div/sqrt is hipcc's default).  tests/test_glsl_math.py
+ * (correctly-rounded f32 div/sqrt is hipcc's default).  tests/test_oracle.py
  * pins each transcendental against libm in double precision (ulp bounds).
  *
  * Shared by: oracle/rt_oracle.cpp (CPU restatement, test infrastructure) and
@@ -83,7 +83,9 @@ RT_HD v3 sub3(v3 a, v3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
 RT_HD v3 mul3(v3 a, v3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
 RT_HD v3 div3(v3 a, v3 b) { return mk3(a.x / b.x, a.y / b.y, a.z / b.z); }
 RT_HD v3 scale3(v3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }   /* a*s and s*a */
-RT_HD v3 divs3(v3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }    /* a/s componentwise */
+/* vec3 / float (hitting.glsl:40, compute.glsl:339): one IEEE reciprocal, then three products
+ * (round 4 definition; GLSL leaves division to 2.5 ulp) */
+RT_HD v3 divs3(v3 a, float s) { const float r = 1.0f / s; return mk3(a.x * r, a.y * r, a.z * r); }
 RT_HD v3 neg3(v3 a) { return mk3(-a.x, -a.y, -a.z); }
 RT_HD float comp3(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 
@@ -94,7 +96,25 @@ RT_HD v3 g_cross(v3 a, v3 b) {
     return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 RT_HD float g_length(v3 a) { return sqrtf(g_dot(a, a)); }
-RT_HD v3 g_normalize(v3 a) { float inv = 1.0f / sqrtf(g_dot(a, a)); return scale3(a, inv); }
+/* GLSL inversesqrt (round 4; GLSL 4.60 §4.7.1 allows 2 ulp): the bit-level first guess
+ * 0x5f375a86 - bits(x)/2 (relative error below 3.5e-2), then three Newton steps
+ * y <- y + y*(1/2 - (x/2)*y*y), fused the same way on both sides (relative error 1.8e-3, 4.6e-6,
+ * then below float rounding: within 2 ulp for normal x, test_oracle.py).  Special inputs as
+ * 1/sqrt(x): +-0 -> +-inf, +inf -> +0, x < 0 and NaN -> NaN.  About a dozen operations where
+ * the IEEE 1/sqrtf(x) takes two correctly rounded operations of ~13 each on gfx950. */
+RT_HD float g_inversesqrt(float x) {
+    float y = rt_u2f(0x5f375a86u - (rt_f2u(x) >> 1));
+    const float h = 0.5f * x;
+    y = fmaf(y, fmaf(-h, y * y, 0.5f), y);
+    y = fmaf(y, fmaf(-h, y * y, 0.5f), y);
+    y = fmaf(y, fmaf(-h, y * y, 0.5f), y);
+    if (x == 0.0f) y = rt_u2f(rt_f2u(x) | 0x7f800000u);   /* +-inf with x's sign */
+    if (x == __builtin_inff()) y = 0.0f;
+    if (!(x >= 0.0f)) y = __builtin_nanf("");              /* x < 0 or NaN (-0 passes: -inf above) */
+    return y;
+}
+/* normalize(a) = a * inversesqrt(dot(a, a)) */
+RT_HD v3 g_normalize(v3 a) { return scale3(a, g_inversesqrt(g_dot(a, a))); }
 /* GLSL reflect(I,N) = I - 2*dot(N,I)*N */
 RT_HD v3 g_reflect(v3 i, v3 n) { float d2 = 2.0f * g_dot(n, i); return sub3(i, scale3(n, d2)); }
 /* GLSL refract(I,N,eta) */

@@ -136,7 +136,7 @@ def rand_sequence(px, py, f, n):
     return out
 
 
-BUILTINS = {"sin": 0, "cos": 1, "log": 2, "acos": 3, "atan2": 4, "fract": 5, "sqrt": 6}
+BUILTINS = {"sin": 0, "cos": 1, "log": 2, "acos": 3, "atan2": 4, "fract": 5, "sqrt": 6, "inversesqrt": 7}
 
 
 def eval_builtin(name, x, y=None):

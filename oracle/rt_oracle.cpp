@@ -875,6 +875,7 @@ void oracle_eval_builtin(int fn, const float* x, const float* y2, float* out, in
             case 4: out[i] = g_atan2(x[i], y2 ? y2[i] : 1.0f); break;
             case 5: out[i] = g_fract(x[i]); break;
             case 6: out[i] = sqrtf(x[i]); break;
+            case 7: out[i] = g_inversesqrt(x[i]); break;
             default: out[i] = 0.0f;
         }
     }

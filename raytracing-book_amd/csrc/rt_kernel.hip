@@ -2433,6 +2433,7 @@ __global__ void eval_builtin_kernel(int fn, const float* __restrict__ x, const f
         case 4: r = g_atan2(x[i], y ? y[i] : 1.0f); break;
         case 5: r = g_fract(x[i]); break;
         case 6: r = sqrtf(x[i]); break;
+        case 7: r = g_inversesqrt(x[i]); break;
         // the leaf tests' division forms (rcp_nr / div_nr) against the compiler's '/'
         case 100: r = x[i] / y[i]; break;
         case 101: r = div_nr(x[i], y[i], rcp_nr(y[i])); break;

@@ -114,7 +114,7 @@ def test_builtins_bit_exact_on_device(gpu):
     rng = np.random.default_rng(0)
     L = rtamd.amd()
     for name, lo, hi in [("sin", -3e5, 3e5), ("cos", -100, 100), ("log", 0, 1), ("acos", -1, 1), ("atan2", -5, 5),
-                         ("fract", -1e4, 1e4), ("sqrt", 0, 1e6)]:
+                         ("fract", -1e4, 1e4), ("sqrt", 0, 1e6), ("inversesqrt", 0, 1e6)]:
         x = rng.uniform(lo, hi, 20000).astype(np.float32)
         # the branch-free special cases (rt_glsl.h g_log, g_sin / g_cos's parity of j): NaN,
         # signed zeros and infinities, negatives, subnormals, arguments past 2^24

@@ -63,6 +63,7 @@ def _ulp_err(got, want):
     ("log", np.log, 1e-6, 1e6, 2.0),
     ("acos", np.arccos, -1.0, 1.0, 3.0),
     ("sqrt", np.sqrt, 0.0, 1e6, 0.5),
+    ("inversesqrt", lambda v: 1.0 / np.sqrt(v), 1e-6, 1e6, 2.0),
 ])
 def test_builtin_accuracy(name, fn, lo, hi, max_ulp):
     """GLSL 4.60 §4.7.1 leaves these driver-defined; ours must stay within a few ulp of float64."""
@@ -93,6 +94,12 @@ def test_builtin_special_cases():
         big = np.array([3.3732712e9, 3.3732714e9, -3.4028235e38, 1e10], np.float32)
         assert np.array_equal(pyoracle.eval_builtin(name, big).view(np.uint32),
                               pyoracle.eval_builtin(name, big).view(np.uint32))
+    # g_inversesqrt's special inputs follow 1/sqrt(x); normal inputs across the whole exponent
+    # range within 2 ulp (unit vectors' dot products sit near 1, the samplers' far from it)
+    r = pyoracle.eval_builtin("inversesqrt", np.array([0.0, -0.0, np.inf, -1.0, np.nan, -np.inf], np.float32))
+    assert r[0] == np.inf and r[1] == -np.inf and r[2] == 0.0 and np.isnan(r[3:]).all()
+    wide = np.exp2(np.random.default_rng(3).uniform(-126, 127, 100000)).astype(np.float32)
+    assert (_ulp_err(pyoracle.eval_builtin("inversesqrt", wide), 1.0 / np.sqrt(wide.astype(np.float64))) <= 2.0).all()
 
 
 def test_builtin_atan2_and_fract():
