@@ -35,9 +35,6 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
  * (types | next address << 8, prims) as uint2.  *n_f4 = its float4 count, 0 when
  * there is no BVH. */
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4);
-/* The same with the node order of option RT_OPTION_TL_ORDER: 0 breadth-first (as above),
- * 1 best-first by estimated visit rate (surface-area ratios; rt_capi.hip build_links). */
-int rt_debug_link_nodes_order(const void* bvh, size_t nbytes, int order, void* out, size_t out_cap, int* n_f4);
 
 /* Host-only: the packed Perlin table rt_upload_texture keeps beside an R32F 6 x 256 texture
  * whose perm columns (3..5) hold whole numbers 0..255: 256 float4 (ranvec x, y, z; the three
@@ -112,11 +109,9 @@ enum {
     RT_OPTION_LEAF_PREFETCH = 20,       /* compact-box kernels: each leaf slot's record loaded
                                            before the prim-type blocks when spheres, boxes
                                            and media are all staged in LDS (1)              */
-    RT_OPTION_TL_GATHER = 21,           /* two-level walk: lanes at global nodes park and
-                                           step together once this many are parked (0) */
-    RT_OPTION_TL_ORDER = 22,            /* link-format node order: 0 breadth-first, 1 best-
-                                           first by estimated visit rate, so the two-level
-                                           walk's LDS prefix follows the large boxes (0) */
+    RT_OPTION_TL_SMALL_LDS = 21,        /* two-level walk: the sphere / compact box records
+                                           staged beside the top levels when each takes at
+                                           most 1/16 of the room (1)                        */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

@@ -14,7 +14,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <queue>
 #include <string>
 #include <vector>
 
@@ -169,8 +168,7 @@ struct rt_ctx {
     int sm_frac = 0;     // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC); 0 = by kernel:
                          // 50 for the compact-box kernels (scene 8 1080p -1.1%, 4K -1.6% against 56), 56 else
                          // (scene 6 +1.4% at 52; profiles/r03_sm_frac_knobs.log)
-    int tl_order = 0;            // link-format node order: 0 breadth-first, 1 best-first by estimated visits (option)
-    int tl_gather = 0;           // two-level walk: gathered global steps once this many lanes park (option)
+    bool tl_small_lds = true;    // two-level walk: small sphere / box tables staged beside the top levels (option)
     bool leaf_prefetch = true;   // leaf records prefetched before the type blocks when all are in LDS (option)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
     bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
@@ -369,56 +367,23 @@ bool boxes_nest(const std::vector<rt_dnode>& dn) {
 // sequence (tests/test_link_nodes.py), and the top levels every ray walks sit at the
 // lowest addresses, the part a two-level launch stages in LDS.  Empty when there is
 // no BVH or it has more nodes than 16-bit indices address.
-// order 1 (option tl_order, for the two-level walk's LDS prefix): best-first instead of
-// breadth-first -- the next node placed is the pending one with the largest estimated visit
-// rate, the product of surface-area ratios child / parent down from the root (the chance a
-// ray through the parent's box meets the child's, for rays spread evenly over directions);
-// ties in placement order.  Every prefix still holds each placed node's parent, so the LDS
-// prefix is a top subtree, but one that follows the large boxes deeper.
-std::vector<float4> build_links(const std::vector<rt_dnode>& dn, int order_mode) {
+std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
     std::vector<float4> out;
     const size_t n = dn.size();
     if (n == 0 || n > RT_LINK_MAX_NODES) return out;
     auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
-    auto area = [&](size_t k) {
-        const double x = (double)dn[k].xmax - dn[k].xmin, y = (double)dn[k].ymax - dn[k].ymin,
-                     z = (double)dn[k].zmax - dn[k].zmin;
-        return x * y + y * z + z * x;
-    };
     std::vector<uint32_t> pos(n, 0xFFFFFFFFu), order;
     order.reserve(n);
-    // pending nodes: (estimated visit rate, -(sequence number), node)
-    typedef std::pair<std::pair<double, long>, uint32_t> Pend;
-    std::priority_queue<Pend> pq;
-    long seq = 0;
-    if (order_mode == 1) pq.push(Pend(std::make_pair(1.0, -seq++), 0u));
-    else order.push_back(0);
-    for (size_t h = 0; order_mode == 1 ? !pq.empty() : h < order.size(); h++) {
-        uint32_t k;
-        double pk = 1.0;
-        if (order_mode == 1) {
-            pk = pq.top().first.first;
-            k = pq.top().second;
-            pq.pop();
-            order.push_back(k);
-        } else {
-            k = order[h];
-        }
+    order.push_back(0);
+    for (size_t h = 0; h < order.size(); h++) {
+        const uint32_t k = order[h];
         if (pos[k] != 0xFFFFFFFFu || order.size() > n) return std::vector<float4>();
         pos[k] = (uint32_t)h;
         if (is_leaf(k)) continue;
         const uint32_t l = k + 1 < n ? (dn[k + 1].meta & 0xFFFFu) : RT_NODE_END;
         if (k + 1 >= n || l == RT_NODE_END || l >= n) return std::vector<float4>();
-        if (order_mode == 1) {
-            const double ak = area(k);
-            for (uint32_t ch : {k + 1, l}) {
-                const double r = ak > 0.0 ? std::min(1.0, area(ch) / ak) : 1.0;
-                pq.push(Pend(std::make_pair(pk * r, -seq++), ch));
-            }
-        } else {
-            order.push_back(k + 1);
-            order.push_back(l);
-        }
+        order.push_back(k + 1);
+        order.push_back(l);
     }
     if (order.size() != n) return out;
     size_t nl = 0;
@@ -987,7 +952,7 @@ int validate(rt_ctx* c) {
     const std::vector<uint8_t>& BB = c->host_buf[RT_BIND_BOXES];
     c->fast = build_fast(c->dnodes, ns, (const rt_quad*)QB.data(), nq, (const rt_box*)BB.data(), nb);
     c->fast.ok = c->fast.ok && c->spec_ok && !c->uv_always;
-    c->links = build_links(c->dnodes, c->tl_order);
+    c->links = build_links(c->dnodes);
     c->pair_leaves = -1;
     c->fast_gen++;
     c->validated = true;
@@ -1623,7 +1588,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.variant = c->variant;
     a.sm_batch = c->sm_batch;
     a.walk_frac = c->walk_frac;
-    a.tl_gather = c->tl_gather;
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);
@@ -1710,8 +1674,13 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         } else if (!fast_walk && a.n_lnode_f4 > 0) {
             if (tl) {
                 // the top levels, then the leaf records (8 B per leaf, read on every leaf visit) when
-                // they take at most half of the room, then the small tables the shading reads
-                const size_t room = cap - perlin_f4 - media_f4;
+                // they take at most half of the room, then the small tables the shading reads, and
+                // the sphere / compact box records when either takes at most 1/16 of the room (a
+                // few nodes' worth; option tl_small_lds)
+                const size_t room0 = cap - perlin_f4 - media_f4;
+                const size_t rsv = (c->tl_small_lds && sph_f4 && 16 * sph_f4 <= room0 ? sph_f4 : 0) +
+                                   (c->tl_small_lds && box_f4 && 16 * box_f4 <= room0 ? box_f4 : 0);
+                const size_t room = room0 - rsv;
                 const size_t lf_f4 = (c->tl_leaf_lds && 2 * leaf_f4 <= room) ? leaf_f4 : 0;
                 a.lds_node_f4 = (int)(std::min(std::min(node_f4, node_cap), room - lf_f4) & ~(size_t)1);
                 at = (size_t)a.lds_node_f4;
@@ -1728,7 +1697,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         if (!fast_walk) {
             if (perlin_f4 && at + perlin_f4 <= cap) { a.perlin_lds = (int)at; at += perlin_f4; }
             if (media_f4 && at + media_f4 <= cap) { a.media_lds = (int)at; at += media_f4; }
-            if (!tl) {
+            if (!tl || c->tl_small_lds) {
                 if (sph_f4 && at + sph_f4 <= cap) { a.sph_lds = (int)at; at += sph_f4; }
                 if (box_f4 && at + box_f4 <= cap) { a.box_cmp_lds = (int)at; at += box_f4; }
             }
@@ -2091,17 +2060,12 @@ int rt_debug_box_records(const void* boxes, size_t nbytes, void* out, size_t out
 }
 
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4) {
-    return rt_debug_link_nodes_order(bvh, nbytes, 0, out, out_cap, n_f4);
-}
-
-int rt_debug_link_nodes_order(const void* bvh, size_t nbytes, int order_mode, void* out, size_t out_cap,
-                              int* n_f4) {
-    if (!bvh || !n_f4 || nbytes % sizeof(rt_bvh_node) || order_mode < 0 || order_mode > 1) return RT_ERR_INVALID_ARG;
+    if (!bvh || !n_f4 || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
     std::vector<rt_dnode> dn;
     rt_ctx tmp;
     int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
     if (r) return r;
-    const std::vector<float4> L = build_links(dn, order_mode);
+    const std::vector<float4> L = build_links(dn);
     *n_f4 = (int)L.size();
     if (out) {
         if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
@@ -2127,7 +2091,7 @@ int rt_debug_sphere_pair_leaves(const void* bvh, size_t nbytes, int* permille) {
     rt_ctx tmp;
     int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
     if (r) return r;
-    *permille = pair_leaves_permille(build_links(dn, 0), (int)dn.size());
+    *permille = pair_leaves_permille(build_links(dn), (int)dn.size());
     return RT_OK;
 }
 
@@ -2233,16 +2197,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SPARSE_STAGE: c->sparse_stage = v != 0; break;
         case RT_OPTION_SPHERE_PAIRS: c->sphere_pairs = v != 0; break;
         case RT_OPTION_LEAF_PREFETCH: c->leaf_prefetch = v != 0; break;
-        case RT_OPTION_TL_GATHER: if (v < 0 || v > 64) return bad(); c->tl_gather = v; break;
-        case RT_OPTION_TL_ORDER:
-            if (v < 0 || v > 1) return bad();
-            if (v != c->tl_order) {   // re-lay the uploaded BVH's link nodes (uploaded again at the next launch)
-                c->tl_order = v;
-                c->links = build_links(c->dnodes, v);
-                c->pair_leaves = -1;
-                c->fast_gen++;
-            }
-            break;
+        case RT_OPTION_TL_SMALL_LDS: c->tl_small_lds = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2278,8 +2233,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_SPARSE_STAGE: *v = c->sparse_stage; break;
         case RT_OPTION_SPHERE_PAIRS: *v = c->sphere_pairs; break;
         case RT_OPTION_LEAF_PREFETCH: *v = c->leaf_prefetch; break;
-        case RT_OPTION_TL_GATHER: *v = c->tl_gather; break;
-        case RT_OPTION_TL_ORDER: *v = c->tl_order; break;
+        case RT_OPTION_TL_SMALL_LDS: *v = c->tl_small_lds; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

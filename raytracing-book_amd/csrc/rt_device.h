@@ -122,8 +122,6 @@ struct rt_kernel_args {
                                  // hold a leaf or ended (64: all of them)
     int leaf_pf;                 // BOXC kernels: the leaf stage prefetches each slot's record (spheres, boxes
                                  // and media all staged in LDS; rt_kernel.hip leaf_prims_t)
-    int tl_gather;               // two-level walk: > 0 gathers the lanes at global nodes and steps them
-                                 // together once this many are parked (link_walk_part_tl); 0 = off
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
     int boxes_canon;             // every box has Box.java's axis-aligned face layout (normal of face i
                                  // along axis z, x, z, x, y, y): planes read as (s_i, w_i)

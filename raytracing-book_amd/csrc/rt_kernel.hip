@@ -800,61 +800,6 @@ __device__ __forceinline__ uint32_t link_walk_part(const NodeSrc& ns, uint32_t n
     return nx;
 }
 
-// link_walk_part for the two-level walk with gathered global steps (option tl_gather = G > 0):
-// a lane whose next node lies in global memory parks there; the wave's LDS walkers go on
-// three steps at a time, and once G lanes are parked (or no LDS walker is left) the parked
-// lanes step together through global nodes until none of them is at one.  A wave then waits
-// on a global read once per gathered step, not on nearly every step (with 64 lanes a few
-// percent of whose steps are global, almost every wave-step has one).  Each lane's node
-// sequence is unchanged.
-template <bool EXACT, bool STATS>
-__device__ __forceinline__ bool node_hit(float4 n0, float4 n1, v3 o, v3 inv, float tmin, float tmax) {
-    if (!EXACT) return aabb_pk(n0, n1, o, inv, tmin, tmax);
-    float lo = tmin, hi = tmax;
-    slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-    slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-    slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-    return !(hi <= lo);
-}
-template <bool EXACT, bool STATS>
-__device__ __forceinline__ uint32_t link_walk_part_tl(const NodeSrc& ns, uint32_t nx, v3 o, v3 inv, float tmin,
-                                                      float tmax, int need, int gather,
-                                                      unsigned long long* st) {
-    for (;;) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            if ((int)nx >= 0 && nx < ns.lim) {
-                if (STATS) {
-                    st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-                    st_small(st, true, ST_NODE_SM);
-                }
-                float4 n0, n1;
-                load_node<STATS, false>(ns, nx, n0, n1);
-                nx = __float_as_uint(node_hit<EXACT, STATS>(n0, n1, o, inv, tmin, tmax) ? n1.z : n1.w);
-            }
-        }
-        const unsigned long long in_lds = __ballot((int)nx >= 0 && nx < ns.lim);
-        unsigned long long in_glob = __ballot((int)nx >= 0 && nx >= ns.lim);
-        if (in_glob != 0 && (in_lds == 0 || __popcll(in_glob) >= gather)) {
-            do {
-                if ((int)nx >= 0 && nx >= ns.lim) {
-                    if (STATS) {
-                        st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-                        st_small(st, true, ST_NODE_SM);
-                    }
-                    const float4* g = reinterpret_cast<const float4*>(ns.gnodes + nx);
-                    const float4 n0 = ldg(g), n1 = ldg(g + 1);
-                    nx = __float_as_uint(node_hit<EXACT, STATS>(n0, n1, o, inv, tmin, tmax) ? n1.z : n1.w);
-                }
-                in_glob = __ballot((int)nx >= 0 && nx >= ns.lim);
-            } while (in_glob != 0);
-        }
-        const unsigned long long walking = __ballot((int)nx >= 0);
-        if (walking == 0 || __popcll(__ballot(1) & ~walking) >= need) break;
-    }
-    return nx;
-}
-
 // compute.glsl:226-266 over the threaded BVH.  Each lane's node sequence is the
 // reference's; only the interleaving of a wave's lanes differs: lanes advance
 // through inner/missed nodes until each holds a hit leaf (or is done), then the
@@ -2186,12 +2131,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             if (status == RT_SM_TRACE) {
                 if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
                 unsigned long long t0 = STATS ? clock64() : 0;
-                if (TL && P.tl_gather > 0) {
-                    const int needw = (__popcll(__ballot(1)) * P.walk_frac + 63) >> 6;
-                    nx = wave_exact
-                             ? link_walk_part_tl<true, STATS>(ns, nx, S.o, inv, 0.001f, tmax, needw, P.tl_gather, st)
-                             : link_walk_part_tl<false, STATS>(ns, nx, S.o, inv, 0.001f, tmax, needw, P.tl_gather, st);
-                } else if (P.walk_frac >= 64) {
+                if (P.walk_frac >= 64) {
                     nx = wave_exact ? link_walk<true, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, st)
                                     : link_walk<false, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, st);
                 } else {

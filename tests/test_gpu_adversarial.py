@@ -85,18 +85,16 @@ def test_scenes_walks_skip_their_spine(gpu, sid, spine):
         assert bit_equal(out, ref), f"{opts}: {mismatch_report(out, ref)}"
 
 
-@pytest.mark.parametrize("tll,gather,order", [(1, 0, 0), (0, 0, 0), (1, 1, 0), (1, 16, 0), (0, 64, 0), (1, 0, 1),
-                                               (1, 16, 1)])
+@pytest.mark.parametrize("tll,small", [(1, 1), (0, 1), (1, 0)])
 @pytest.mark.parametrize("cap", [4096, 32768, 65536])
-def test_two_level_walk_forced(gpu, cap, tll, gather, order):
+def test_two_level_walk_forced(gpu, cap, tll, small):
     """The ~4000-node cloud, which fits LDS, with only `cap` bytes of its nodes staged, its
-    leaf records in LDS (tll 1) or global memory, its global steps taken per lane or gathered
-    (option tl_gather: lanes park at global nodes until `gather` of them wait), and its nodes
-    breadth-first or best-first (option tl_order): the same bits as the oracle whatever the
-    split between LDS and global nodes."""
+    leaf records in LDS (tll 1) or global memory, and its 8 boxes' records in LDS (option
+    tl_small_lds) or global memory: the same bits as the oracle whatever the split between
+    LDS and global nodes."""
     case = next(c for c in CASES if c.name == "bvh_4k_lds")
     ref = oracle(case)
-    out, info = render(case, {"lds_node_cap": cap, "tl_leaf_lds": tll, "tl_gather": gather, "tl_order": order})
+    out, info = render(case, {"lds_node_cap": cap, "tl_leaf_lds": tll, "tl_small_lds": small})
     assert info["shape_name"] == "link-two-level" and info["lds_nodes"] == cap // 32, info
     assert bit_equal(out, ref), mismatch_report(out, ref)
 

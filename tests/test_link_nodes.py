@@ -23,17 +23,13 @@ from test_fast_tables import END, is_leaf, threaded
 LEAF, LEND, NEXT_END = 0x80000000, 0xFFFFFFFF, 0xFFFFFF
 
 
-def links_of(bvh_bytes, order=None):
+def links_of(bvh_bytes):
     L = rtamd.amd()
     bvh = ctypes.create_string_buffer(bvh_bytes, len(bvh_bytes))
     n = ctypes.c_int()
-    if order is None:
-        call = lambda o, cap: L.rt_debug_link_nodes(bvh, len(bvh_bytes), o, cap, ctypes.byref(n))
-    else:
-        call = lambda o, cap: L.rt_debug_link_nodes_order(bvh, len(bvh_bytes), order, o, cap, ctypes.byref(n))
-    assert call(None, 0) == 0
+    assert L.rt_debug_link_nodes(bvh, len(bvh_bytes), None, 0, ctypes.byref(n)) == 0
     out = np.zeros((max(n.value, 1), 4), np.float32)
-    assert call(out.ctypes.data, out.nbytes) == 0
+    assert L.rt_debug_link_nodes(bvh, len(bvh_bytes), out.ctypes.data, out.nbytes, ctypes.byref(n)) == 0
     return out[:n.value]
 
 
@@ -56,28 +52,6 @@ def bfs_order(tn):
         h += 1
         if not is_leaf(tn[k]):
             order += [k + 1, int(tn[k + 1]["meta"]) & 0xFFFF]
-    return order
-
-
-def best_first_order(tn):
-    """Option tl_order 1: the pending node with the largest estimated visit rate next (the
-    product of surface-area ratios child / parent from the root), ties in placement order."""
-    import heapq
-    def area(k):
-        b = [float(v) for v in tn[k]["box"]]
-        x, y, z = b[1] - b[0], b[3] - b[2], b[5] - b[4]
-        return x * y + y * z + z * x
-    heap, seq, order = [(-1.0, 0, 0)], 1, []
-    while heap:
-        negp, _, k = heapq.heappop(heap)
-        order.append(k)
-        if is_leaf(tn[k]):
-            continue
-        ak = area(k)
-        for ch in (k + 1, int(tn[k + 1]["meta"]) & 0xFFFF):
-            r = min(1.0, area(ch) / ak) if ak > 0.0 else 1.0
-            heapq.heappush(heap, (-(-negp * r), seq, ch))
-            seq += 1
     return order
 
 
@@ -117,9 +91,9 @@ def walk_links(ln, n, hits, node_of_slot):
     return seen, tested
 
 
-def check_layout(tn, ln, order=None):
+def check_layout(tn, ln):
     n = len(tn)
-    order = bfs_order(tn) if order is None else order
+    order = bfs_order(tn)
     assert sorted(order) == list(range(n))
     pos = np.empty(n, np.int64)
     pos[order] = np.arange(n)
@@ -186,31 +160,5 @@ def test_link_format_reaches_the_16_bit_node_limit(n_leaves):
     if n_leaves <= 4096:
         rng = np.random.default_rng(n_leaves)
         for p in (0.5, 0.9, 1.0):
-            hits = rng.random(len(tn)) < p
-            assert walk_links(ln, len(tn), hits, order) == walk_threaded(tn, hits)
-
-
-@pytest.mark.parametrize("sid", [0, 6, 8])
-def test_best_first_link_order(sid):
-    """Option tl_order 1 (the two-level walk's LDS prefix by estimated visit rate): the nodes in
-    best-first order, every prefix holding each node's parent (a top subtree), successors
-    rewritten to the new addresses, and the walk replaying the threaded walk under random hits."""
-    scene = rtamd.Scene(sid, 64, 36, seed=1)
-    tn = threaded(scene)
-    order = best_first_order(tn)
-    ln = links_of(scene.buffers[1], order=1)
-    assert check_layout(tn, ln, order) == order
-    assert np.array_equal(links_of(scene.buffers[1], order=0).view(np.uint32), links_of(scene.buffers[1]).view(np.uint32))
-    parent = {}
-    for k, nd in enumerate(tn):
-        if not is_leaf(nd):
-            parent[k + 1] = parent[int(tn[k + 1]["meta"]) & 0xFFFF] = k
-    placed = set()
-    for k in order:
-        assert k == 0 or parent[k] in placed
-        placed.add(k)
-    rng = np.random.default_rng(sid + 100)
-    for p in (0.3, 0.7, 1.0):
-        for _ in range(10):
             hits = rng.random(len(tn)) < p
             assert walk_links(ln, len(tn), hits, order) == walk_threaded(tn, hits)

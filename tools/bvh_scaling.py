@@ -6,7 +6,7 @@ colour fold).  For the ~4000-node cloud, which fits LDS (one 1024-thread workgro
 the same scene is also rendered with only part of its nodes staged (RT_OPTION_LDS_NODE_CAP:
 the two-level walk reads the rest from global memory), so the cost of the two-level walk is
 measured on identical work; the ~9800-node cloud needs it by default.
-usage: python tools/bvh_scaling.py [--gather 0,16]   (option tl_gather values for the two-level rows)
+usage: python tools/bvh_scaling.py [--sizes 4000,9000] [--caps 130048,32768] [--extra '{"tl_small_lds": 0}']
 """
 import argparse
 import json
@@ -42,46 +42,40 @@ def timed(scene, options, reps=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gather", default="0", help="comma-separated tl_gather values for the two-level rows")
-    ap.add_argument("--orders", default="0", help="comma-separated tl_order values (link node order) for the two-level rows")
     ap.add_argument("--no-tll0", action="store_true", help="skip the rows with the leaf records in global memory")
     ap.add_argument("--sizes", default="2000,4000,9000")
+    ap.add_argument("--extra", default="{}", help="JSON options added to every row's context (e.g. '{\"tl_small_lds\": 0}')")
+    ap.add_argument("--caps", default="98304,65536,32768,8192", help="forced LDS node caps (bytes) for the 4000 cloud")
     args = ap.parse_args()
-    gathers = [int(g) for g in args.gather.split(",")]
-    orders = [int(o) for o in args.orders.split(",")]
     sizes = [int(x) for x in args.sizes.split(",")]
+    extra = json.loads(args.extra)
     rows = []
     for n, seed in ((2000, 2), (4000, 4), (9000, 9)):
         if n not in sizes:
             continue
         sc = adversarial.sphere_cloud(n, seed, W=W, H=H)
-        caps = [0] if n != 4000 else [0, 98304, 65536, 32768, 8192]
+        caps = [0] if n != 4000 else [0] + [int(c) for c in args.caps.split(",")]
         for cap in caps:
             two_level = bool(cap) or n == 9000
             # the two-level walk with its leaf records in LDS (default) and in global memory
             for tll in ((1, 0) if two_level and not args.no_tll0 else (1,)):
-                for g, order in ([(g, o) for o in orders for g in gathers] if two_level else [(0, 0)]):
-                    opts = {"lds_node_cap": cap} if cap else {}
-                    if order:
-                        opts["tl_order"] = order
-                    if not tll:
-                        opts["tl_leaf_lds"] = 0
-                    if g:
-                        opts["tl_gather"] = g
-                    rate, ms, info = timed(sc, opts)
-                    row = {"spheres": n, "bvh_nodes": sc.info["n_bvh_nodes"], "lds_node_cap": cap, "tl_leaf_lds": tll,
-                           "tl_gather": g, "tl_order": order, "Msamples_s": round(rate, 1), "ms_per_launch": round(ms, 3),
-                           "shape": info["shape_name"], "block": info["block"], "lds_nodes": info["lds_nodes"],
-                           "lds_bytes": info["lds_bytes"]}
-                    rows.append(row)
-                    print(json.dumps(row), flush=True)
+                opts = {"lds_node_cap": cap} if cap else {}
+                opts.update(extra)
+                if not tll:
+                    opts["tl_leaf_lds"] = 0
+                rate, ms, info = timed(sc, opts)
+                row = {"spheres": n, "bvh_nodes": sc.info["n_bvh_nodes"], "lds_node_cap": cap, "tl_leaf_lds": tll,
+                       "Msamples_s": round(rate, 1), "ms_per_launch": round(ms, 3), "shape": info["shape_name"],
+                       "block": info["block"], "lds_nodes": info["lds_nodes"], "lds_bytes": info["lds_bytes"],
+                       "extra": extra}
+                rows.append(row)
+                print(json.dumps(row), flush=True)
     if 4000 in sizes:
         base = next(r for r in rows if r["spheres"] == 4000 and r["lds_node_cap"] == 0)["Msamples_s"]
         for r in rows:
             if r["spheres"] == 4000:
                 print(json.dumps({"spheres": 4000, "lds_node_cap": r["lds_node_cap"], "tl_leaf_lds": r["tl_leaf_lds"],
-                                  "tl_gather": r["tl_gather"], "tl_order": r["tl_order"],
-                                  "cost_vs_all_in_lds": round(base / r["Msamples_s"], 3)}),
+                                  "extra": extra, "cost_vs_all_in_lds": round(base / r["Msamples_s"], 3)}),
                       flush=True)
 
 

@@ -26,9 +26,16 @@ def main():
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--options", default="{}", help='JSON, e.g. {"leaf_defer": 16}')
+    ap.add_argument("--cloud", type=int, default=0, help="N > 0: tests/adversarial.py sphere_cloud(N) instead of --scene")
     a = ap.parse_args()
     import json
-    scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
+    if a.cloud:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import adversarial
+        seeds = {2000: 2, 4000: 4, 9000: 9}
+        scene = adversarial.sphere_cloud(a.cloud, seeds.get(a.cloud, 1), W=a.width, H=a.height)
+    else:
+        scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
     ctx = rtamd.RenderContext(devices=(0,), ab=True, options=json.loads(a.options) or None)   # the stats kernels are in the A/B build
     ctx.upload_scene(scene)
     ctx.set_params(max_depth=a.depth, spp=4096)
@@ -42,7 +49,7 @@ def main():
     v = {n: buf[i] for i, n in enumerate(NAMES)}
     tot = v["TOTAL"] or 1
     samples = a.width * a.height * a.frames
-    print(f"scene {a.scene} {a.width}x{a.height}x{a.frames}: {samples} samples, wave-cycles total {tot:.3e}")
+    print(f"{'cloud ' + str(a.cloud) if a.cloud else 'scene ' + str(a.scene)} {json.loads(a.options)} {a.width}x{a.height}x{a.frames}: {samples} samples, wave-cycles total {tot:.3e}")
     for reg in ["START", "NODE", "LEAF", "SHADE"]:
         cyc, it, ln = v[reg + "_CYC"], v[reg + "_IT"], v[reg + "_LN"]
         util = ln / (64.0 * it) if it else 0
