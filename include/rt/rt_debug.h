@@ -112,6 +112,9 @@ enum {
     RT_OPTION_TL_SMALL_LDS = 21,        /* two-level walk: the sphere / compact box records
                                            staged beside the top levels when each takes at
                                            most 1/16 of the room (1)                        */
+    RT_OPTION_SHADE_LDS = 22,           /* shading tables in LDS: sphere and compact box
+                                           materials, texture descriptors, small texture
+                                           slots (1)                                        */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

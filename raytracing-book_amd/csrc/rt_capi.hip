@@ -168,6 +168,8 @@ struct rt_ctx {
     int sm_frac = 0;     // ... or fraction of the lanes with a walk, in 64ths (env RT_SM_FRAC); 0 = by kernel:
                          // 50 for the compact-box kernels (scene 8 1080p -1.1%, 4K -1.6% against 56), 56 else
                          // (scene 6 +1.4% at 52; profiles/r03_sm_frac_knobs.log)
+    bool shade_lds = true;       // shading tables in LDS (sphere / box materials, small textures; option):
+                                 // scenes 8 / 0 / 6 -0.3 / -1.0 / -1.2% (profiles/r04_shade_lds_ab_s*.log)
     bool tl_small_lds = true;    // two-level walk: small sphere / box tables staged beside the top levels (option)
     bool leaf_prefetch = true;   // leaf records prefetched before the type blocks when all are in LDS (option)
     int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
@@ -803,7 +805,20 @@ bool compact_box(const rt_quad* Q, float4 out[3]) {
     const float sz = Q[0].normal[2], sx = Q[1].normal[0], sy = Q[4].normal[1];
     out[0] = make_float4(mnx, mny, mnz, mxx);
     out[1] = make_float4(mxy, mxz, sz, sx);
-    out[2] = make_float4(sy, 0.0f, 0.0f, 0.0f);
+    // z: quads[0]'s texture id, w: the sign bits of each face normal's two zero components
+    // (bits 2i, 2i+1: components (axis+1)%3, (axis+2)%3 of face i), so the shading can rebuild
+    // every face normal's exact bits from the record (rt_kernel.hip boxc_normal)
+    uint32_t zmask = 0;
+    {
+        static const int kAxS[6] = {2, 0, 2, 0, 1, 1};
+        for (int i = 0; i < 6; i++)
+            for (int j = 1; j <= 2; j++)
+                if (std::signbit(Q[i].normal[(kAxS[i] + j) % 3])) zmask |= 1u << (2 * i + j - 1);
+    }
+    float texf, zmf;
+    std::memcpy(&texf, &Q[0].texture_id, 4);
+    std::memcpy(&zmf, &zmask, 4);
+    out[2] = make_float4(sy, 0.0f, texf, zmf);
     static const int kAx[6] = {2, 0, 2, 0, 1, 1};   // Box.java:32-37 face order: normals along z, x, z, x, y, y
     const float sv[6] = {sz, sx, -sz, -sx, sy, -sy};
     const float qk[6] = {mxz, mxx, mnz, mnx, mxy, mny};
@@ -1669,6 +1684,8 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         a.lds_node_f4 = 0;
         a.leaf_lds = -1;
         a.perlin_lds = a.media_lds = a.sph_lds = a.box_cmp_lds = -1;
+        a.sph_mat_lds = a.box_mat_lds = a.tex_lds = -1;
+        for (int t = 0; t < 8; t++) a.tex_lds_off[t] = -1;
         if (meta) {
             at = node_f4;   // the threaded nodes (32 B each) from address 0 (rt_launch_render: META_LDS)
         } else if (!fast_walk && a.n_lnode_f4 > 0) {
@@ -1700,6 +1717,35 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             if (!tl || c->tl_small_lds) {
                 if (sph_f4 && at + sph_f4 <= cap) { a.sph_lds = (int)at; at += sph_f4; }
                 if (box_f4 && at + box_f4 <= cap) { a.box_cmp_lds = (int)at; at += box_f4; }
+            }
+            // the shading tables (option shade_lds): every sphere's third float4, every compact
+            // box's (emission, material), the texture slots' descriptors and the texels of the
+            // small slots (at most 1024 words: the solid and checker colour tables), each when
+            // it fits -- so a hit's material, texture and colour need no global read
+            if (c->shade_lds && pooled && !tl) {
+                if (a.sph_lds >= 0 && at + (size_t)n_sph <= cap) { a.sph_mat_lds = (int)at; at += (size_t)n_sph; }
+                if (a.box_cmp_lds >= 0 && a.box_all_cmp && at + (size_t)n_box <= cap) {
+                    a.box_mat_lds = (int)at;
+                    at += (size_t)n_box;
+                }
+                size_t need = 8;
+                for (int t = 0; t < 8; t++) {
+                    const size_t words = (size_t)c->tex_w[t] * (size_t)c->tex_h[t];
+                    if (c->tex_w[t] > 0 && c->tex_h[t] > 0 && words <= 1024) need += (words + 3) / 4;
+                }
+                if (at + need <= cap) {
+                    a.tex_lds = (int)at;
+                    size_t off = at + 8;
+                    for (int t = 0; t < 8; t++) {
+                        const size_t words = (size_t)c->tex_w[t] * (size_t)c->tex_h[t];
+                        a.tex_lds_off[t] = -1;
+                        if (c->tex_w[t] > 0 && c->tex_h[t] > 0 && words <= 1024) {
+                            a.tex_lds_off[t] = (int)off;
+                            off += (words + 3) / 4;
+                        }
+                    }
+                    at = off;
+                }
             }
         }
         a.lds_end_f4 = (int)at;
@@ -2198,6 +2244,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SPHERE_PAIRS: c->sphere_pairs = v != 0; break;
         case RT_OPTION_LEAF_PREFETCH: c->leaf_prefetch = v != 0; break;
         case RT_OPTION_TL_SMALL_LDS: c->tl_small_lds = v != 0; break;
+        case RT_OPTION_SHADE_LDS: c->shade_lds = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2234,6 +2281,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_SPHERE_PAIRS: *v = c->sphere_pairs; break;
         case RT_OPTION_LEAF_PREFETCH: *v = c->leaf_prefetch; break;
         case RT_OPTION_TL_SMALL_LDS: *v = c->tl_small_lds; break;
+        case RT_OPTION_SHADE_LDS: *v = c->shade_lds; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

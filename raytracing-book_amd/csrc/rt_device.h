@@ -139,6 +139,12 @@ struct rt_kernel_args {
     int sph_lds;                 // float4 offset of the spheres' intersection halves (A, B) in LDS, or -1
     int n_sph_lds;               // spheres staged there
     int n_box_lds;               // boxes whose compact records are staged (all of them)
+    // shading tables in LDS (option shade_lds; rt_kernel.hip shade / texture_color), each -1 when absent:
+    int sph_mat_lds;             // per sphere its third float4 (emission, material)
+    int box_mat_lds;             // per compact box (quads[0] emission, material); texture id and the
+                                 // faces' zero-sign bits ride in its compact record (rt_capi.hip compact_box)
+    int tex_lds;                 // 8 int4 per texture slot: (w, h, is_float, float4 offset of its texels or -1)
+    int tex_lds_off[8];          // host side of the same offsets (the staging loop reads them)
     int block;                   // the render kernel's workgroup size: 512, or 1024 (one per CU) when the
                                  // records above fit its LDS (RT_LDS_BIG_BYTES)
     int acc_lds;                 // float4 offset of the lanes' running-mean slots (after everything staged)
@@ -182,7 +188,7 @@ struct rt_kernel_args {
 
 // What rt_launch_render launched (rt_debug_last_launch)
 enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
-       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_LEAF_PF, RT_LI_N = 16 };
+       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_LEAF_PF, RT_LI_SHADE_LDS, RT_LI_N = 16 };
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)

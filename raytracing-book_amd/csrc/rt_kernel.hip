@@ -919,6 +919,28 @@ __device__ __forceinline__ void texel_in(const rt_dtex& T, int x, int y, float o
     out[1] = T.is_float ? 0.0f : unorm8_fast((c >> 8) & 0xFFu);
     out[2] = T.is_float ? 0.0f : unorm8_fast((c >> 16) & 0xFFu);
 }
+// texel() of slot `slot` through the LDS shading table when it is staged (P.tex_lds: the slot's
+// (w, h, is_float, texel offset); the same words as the texture), else from global memory
+__device__ __forceinline__ void texel_slot(const KP& P, int slot, int x, int y, float out[3]) {
+    if (P.tex_lds >= 0) {
+        const float4 dsc = rt_dyn_lds[P.tex_lds + slot];
+        const int w = __float_as_int(dsc.x), h = __float_as_int(dsc.y), off = __float_as_int(dsc.w);
+        if (off >= 0) {
+            out[0] = out[1] = out[2] = 0.0f;
+            if (x < 0 || y < 0 || x >= w || y >= h) return;
+            const uint32_t c = reinterpret_cast<const uint32_t*>(rt_dyn_lds + off)[y * w + x];
+            if (__float_as_int(dsc.z)) {
+                out[0] = __uint_as_float(c);
+            } else {
+                out[0] = unorm8_fast(c & 0xFFu);
+                out[1] = unorm8_fast((c >> 8) & 0xFFu);
+                out[2] = unorm8_fast((c >> 16) & 0xFFu);
+            }
+            return;
+        }
+    }
+    texel(P.tex[slot], x, y, out);
+}
 __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
     float t[3];
     texel(T, x, y, t);
@@ -1057,8 +1079,16 @@ __device__ __forceinline__ v2 resolve_uv(const KP& P, const UvSrc& s, float time
     int kind = s.kind_idx >> 16;
     if (kind == 2) { v2 r = {s.a, s.b}; return r; }
     if (kind == 1) {
-        const float4* sp = reinterpret_cast<const float4*>(P.spheres + (s.kind_idx & 0xFFFF));
-        float4 A = ldg(sp), B = ldg(sp + 1);
+        const int si = s.kind_idx & 0xFFFF;
+        float4 A, B;
+        if (P.sph_mat_lds >= 0) {   // the shading tables are on: the sphere's (A, B) from LDS
+            A = rt_dyn_lds[P.sph_lds + 2 * si];
+            B = rt_dyn_lds[P.sph_lds + 2 * si + 1];
+        } else {
+            const float4* sp = reinterpret_cast<const float4*>(P.spheres + si);
+            A = ldg(sp);
+            B = ldg(sp + 1);
+        }
         v3 center = add3(f3(A), scale3(f3(B), time));
         return sphere_uv(sub3(mk3(s.a, s.b, s.c), center));
     }
@@ -1075,16 +1105,17 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
     const rt_dtex& T = P.tex[index & 7];
     float t[3];
     if (type == RT_TEXTYPE_SOLID) {
-        texel(T, detail_i, 0, t);
+        texel_slot(P, index & 7, detail_i, 0, t);
         return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_CHECKER) {   // :6-17
         int pix = detail_i * 3;
-        float scale = texel_r(T, pix + 2, 0);
+        texel_slot(P, index & 7, pix + 2, 0, t);
+        float scale = t[0];
         float inv_scale = 1.0f / scale;
         v3 q = scale3(p, inv_scale);
         int s = rt_f2i(q.x) + rt_f2i(q.y) + rt_f2i(q.z);
-        texel(T, (s % 2 == 0) ? pix : pix + 1, 0, t);
+        texel_slot(P, index & 7, (s % 2 == 0) ? pix : pix + 1, 0, t);
         return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_PERLIN) {    // :79-94
@@ -1510,7 +1541,16 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     const int h_type = h.tif & 0xF, h_face = (h.tif >> 4) & 0x7, h_idx = (int)((unsigned)h.tif >> 16);
     if (h_type == RT_MODEL_SPHERE) {   // hitting.glsl:40-42 + compute.glsl:199-204
         const float4* sp = reinterpret_cast<const float4*>(P.spheres + h_idx);
-        float4 A = ldg(sp), B = ldg(sp + 1), C = ldg(sp + 2);
+        float4 A, B, C;
+        if (P.sph_mat_lds >= 0) {   // the shading tables: the whole record from LDS
+            A = rt_dyn_lds[P.sph_lds + 2 * h_idx];
+            B = rt_dyn_lds[P.sph_lds + 2 * h_idx + 1];
+            C = rt_dyn_lds[P.sph_mat_lds + h_idx];
+        } else {
+            A = ldg(sp);
+            B = ldg(sp + 1);
+            C = ldg(sp + 2);
+        }
         v3 center = add3(f3(A), scale3(f3(B), S.time));
         v3 on = divs3(sub3(p, center), B.w);
         front = g_dot(d, on) < 0.0f;
@@ -1523,6 +1563,25 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         front = true;
         material = ldg_i(&P.media[h_idx].phase_material);
         tex_id = ldg_i(&P.media[h_idx].texture_id);
+    } else if (h_type == RT_MODEL_BOX && P.box_mat_lds >= 0) {
+        // a compact box from the shading tables: face h_face's normal rebuilt bit for bit from the
+        // compact record (canonical axis and value, the zero components' signs in c2.w), material,
+        // texture and emission of quads[0] (compute.glsl:217-221)
+        const float4* cr = rt_dyn_lds + P.box_cmp_lds + RT_BOXC_F4 * h_idx;
+        const float4 c1 = cr[1], c2 = cr[2];
+        const float4 bm = rt_dyn_lds[P.box_mat_lds + h_idx];
+        const float sval = h_face == 0 ? c1.z : h_face == 1 ? c1.w : h_face == 2 ? -c1.z
+                         : h_face == 3 ? -c1.w : h_face == 4 ? c2.x : -c2.x;
+        const int ax = (h_face == 0 || h_face == 2) ? 2 : (h_face == 1 || h_face == 3) ? 0 : 1;
+        const uint32_t zm = (uint32_t)__float_as_int(c2.w) >> (2 * h_face);
+        const float z1 = __uint_as_float((zm & 1u) << 31), z2 = __uint_as_float(((zm >> 1) & 1u) << 31);
+        // components (ax+1)%3 and (ax+2)%3 are the zeros
+        v3 n = ax == 0 ? mk3(sval, z1, z2) : ax == 1 ? mk3(z2, sval, z1) : mk3(z1, z2, sval);
+        front = g_dot(d, n) < 0.0f;
+        normal = front ? n : neg3(n);
+        material = __float_as_int(bm.w);
+        tex_id = __float_as_int(c2.z);
+        if (front) emis = mk3(bm.x, bm.y, bm.z);
     } else {   // quad, or box face h_face (material from quads[0], compute.glsl:217-221)
         const float4* q0 = (h_type == RT_MODEL_QUAD) ? reinterpret_cast<const float4*>(P.quads + h_idx)
                                                     : reinterpret_cast<const float4*>(P.boxes + h_idx);
@@ -2278,6 +2337,34 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
         }
         if (P.box_cmp_lds >= 0)   // the boxes' compact records (box_test_compact)
             for (int k = tid; k < RT_BOXC_F4 * P.n_box_lds; k += BLOCK) s_nodes[P.box_cmp_lds + k] = ldg(P.dboxc + k);
+        // the shading tables (P.sph_mat_lds / box_mat_lds / tex_lds, option shade_lds)
+        if (P.sph_mat_lds >= 0) {   // per sphere its third float4: emission, material
+            const float4* sp = reinterpret_cast<const float4*>(P.spheres);
+            for (int k = tid; k < P.n_sph_lds; k += BLOCK) s_nodes[P.sph_mat_lds + k] = ldg(sp + 3 * k + 2);
+        }
+        if (P.box_mat_lds >= 0) {   // per box quads[0]'s emission and material
+            for (int k = tid; k < P.n_box_lds; k += BLOCK) {
+                const float4* q0 = reinterpret_cast<const float4*>(P.boxes + k);
+                const float4 e = ldg(q0 + 4), m = ldg(q0 + 1);
+                s_nodes[P.box_mat_lds + k] = make_float4(e.x, e.y, e.z, m.w);
+            }
+        }
+        if (P.tex_lds >= 0) {   // per slot (w, h, is_float, texel offset), then the small slots' texels
+            if (tid < 8) {
+                const rt_dtex& T = P.tex[tid];
+                const int off = T.data ? P.tex_lds_off[tid] : -1;
+                s_nodes[P.tex_lds + tid] = make_float4(__int_as_float(T.data ? T.w : 0), __int_as_float(T.h),
+                                                       __int_as_float(T.is_float), __int_as_float(off));
+            }
+            for (int t = 0; t < 8; t++) {
+                const rt_dtex& T = P.tex[t];
+                if (P.tex_lds_off[t] < 0 || !T.data) continue;
+                const int words = T.w * T.h;
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(T.data);
+                uint32_t* dst = reinterpret_cast<uint32_t*>(s_nodes + P.tex_lds_off[t]);
+                for (int k = tid; k < words; k += BLOCK) dst[k] = src[k];
+            }
+        }
     }
     // per lane: the pixel's running mean during a unit, after what this launch
     // shape stages (P.acc_lds, set by rt_launch_render with the LDS size)
@@ -2507,6 +2594,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
     if (shape == FAST_LDS || shape == FAST_GLOBAL || shape == META_GLOBAL) {   // nothing else staged
         if (shape == META_GLOBAL) staged = 0;
         a.perlin_lds = a.media_lds = a.sph_lds = a.box_cmp_lds = -1;
+        a.sph_mat_lds = a.box_mat_lds = a.tex_lds = -1;
     }
 #endif
     if ((shape == LINK_LDS || shape == LINK_TL) && staged > (a.block == 1024 ? RT_LDS_BIG_BYTES : RT_LDS_DYN_BYTES))
@@ -2533,6 +2621,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         info[RT_LI_SPARSE] = a.samples && a.sflags ? 1 : 0;
         info[RT_LI_SPAIR] = (pool && shape == LINK_LDS && a.sph_pairs && !a.box_all_cmp && a.sph_lds >= 0) ? 1 : 0;
         info[RT_LI_LEAF_PF] = (pool && (shape == LINK_LDS || shape == LINK_TL)) ? a.leaf_pf : 0;
+        info[RT_LI_SHADE_LDS] = (a.sph_mat_lds >= 0) + 2 * (a.box_mat_lds >= 0) + 4 * (a.tex_lds >= 0);
     }
     // Arguments live in device memory: the by-value kernarg struct would be copied
     // to scratch as soon as a non-inlined device function takes its address.

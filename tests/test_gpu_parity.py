@@ -67,6 +67,27 @@ def test_leaf_record_prefetch_matches_oracle(gpu, scene_id, want):
         assert bit_equal(out, ref), f"{opts}: {mismatch_report(out, ref)}"
 
 
+@pytest.mark.parametrize("shade", [1, 0])
+@pytest.mark.parametrize("scene_id,w,h,frames,depth", CASES)
+def test_shading_tables_match_oracle(gpu, scene_id, w, h, frames, depth, shade):
+    """The shading tables in LDS (option shade_lds, default on: sphere records' third float4,
+    compact boxes' materials with their face normals rebuilt from the compact record, texture
+    descriptors and the small texture slots) and the records read from global memory (off):
+    every scene bit for bit against the oracle; scene 8 stages all three tables (asserted)."""
+    s = rtamd.Scene(scene_id, w, h, seed=1)
+    ref = oracle_image(s, frames, max_depth=depth)
+    ctx = rtamd.RenderContext(options={"shade_lds": shade})
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=depth, spp=frames)
+    ctx.resize(w, h)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, frames))
+    out, info = ctx.read_image(), ctx.last_launch()
+    ctx.close()
+    if scene_id == 8 or not shade:
+        assert info["shade_lds"] == 7 * shade, info
+    assert bit_equal(out, ref), f"shade_lds {info['shade_lds']}: {mismatch_report(out, ref)}"
+
+
 @pytest.mark.parametrize("scene_id,pairs", [(0, 1), (1, 1), (9, 1), (8, 0), (6, 0)])
 def test_sphere_pair_kernel_matches_oracle(gpu, scene_id, pairs):
     """Scenes whose leaves are mostly two spheres take the kernels that test both at once
