@@ -89,7 +89,7 @@ enum {
     RT_OPTION_SM_BATCH = 8,             /* shading batch, lanes (64)                        */
     RT_OPTION_SM_FRAC = 9,              /* shading batch, 64ths of the walking lanes (0 =   
                                            by kernel: 50 compact-box kernels, else 56)      */
-    RT_OPTION_WALK_FRAC = 10,           /* partial node walks, 64ths (48)                   */
+    RT_OPTION_WALK_FRAC = 10,           /* partial node walks, 64ths (0: by BVH size)       */
     RT_OPTION_WATCHDOG_MS = 11,         /* a wave that stores no sample for this long sets
                                            the fault word and leaves (120000); 0 = at once  */
     RT_OPTION_CHUNK_WAIT_MS = 12,       /* ordered-chunk wait bound (30000); 0 = at once    */

@@ -172,7 +172,8 @@ struct rt_ctx {
                                  // scenes 8 / 0 / 6 -0.3 / -1.0 / -1.2% (profiles/r04_shade_lds_ab_s*.log)
     bool tl_small_lds = true;    // two-level walk: small sphere / box tables staged beside the top levels (option)
     bool leaf_prefetch = true;   // leaf records prefetched before the type blocks when all are in LDS (option)
-    int walk_frac = 48;  // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC)
+    int walk_frac = 0;   // render_stream: node walks stop at this fraction of lanes ready, in 64ths (env RT_WALK_FRAC);
+                         // 0 = by BVH size: 8 up to 64 nodes, 32 up to 1024, 48 above (walk_frac_for)
     bool big_wg = true;    // 1024-thread workgroups with sphere + box records in LDS when they fit (env RT_BIG_WG=0: A/B)
     bool sph_lds = true;   // sphere records' first two float4 in LDS when they fit (env RT_SPH_LDS=0 disables; A/B)
     bool compact_boxes = true;   // boxes' compact records when every box has one (box_test_compact; option 0: A/B)
@@ -416,6 +417,14 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
     }
     return out;
 }
+
+// The default walk round threshold (option walk_frac 0): a round's node walk stops once this
+// many 64ths of its lanes hold a leaf or ended.  Measured per scene (round 4,
+// profiles/r04_knobs*_s*.log; the default was 48 for every scene): the 7-node Cornell boxes
+// want short rounds (scene 6: 8..16 -6%, scene 7: 8 -8.6%, 16 -2.5%), scene 0's 511 nodes 32..36
+// (-1.3%), scene 8's 1793 nodes 48..52 (44: +0.4%).  Rounds only regroup which lanes walk and
+// test leaves together: every lane's node and prim sequence is unchanged (bit-identical).
+int walk_frac_for(int n_nodes) { return n_nodes <= 64 ? 8 : n_nodes <= 1024 ? 32 : 48; }
 
 // The spine of the link-format walk (rt_kernel.hip spine_entry): every walk starts at the
 // root and, while it hits, goes on to the right child (compute.glsl:259-260), so its first
@@ -1602,7 +1611,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                     : 0;
     a.variant = c->variant;
     a.sm_batch = c->sm_batch;
-    a.walk_frac = c->walk_frac;
+    a.walk_frac = c->walk_frac ? c->walk_frac : walk_frac_for(c->n_dnodes);
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);
@@ -2250,7 +2259,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
         case RT_OPTION_SM_BATCH: if (v < 1 || v > 64) return bad(); c->sm_batch = v; break;
         case RT_OPTION_SM_FRAC: if (v < 0 || v > 64) return bad(); c->sm_frac = v; break;
-        case RT_OPTION_WALK_FRAC: if (v < 1 || v > 64) return bad(); c->walk_frac = v; break;
+        case RT_OPTION_WALK_FRAC: if (v < 0 || v > 64) return bad(); c->walk_frac = v; break;
         case RT_OPTION_WATCHDOG_MS: if (v < 0) return bad(); c->watchdog_ticks = (unsigned long long)v * 100000ull; break;
         case RT_OPTION_CHUNK_WAIT_MS: if (v < 0) return bad(); c->chunk_wait_ticks = (unsigned long long)v * 100000ull; break;
         case RT_OPTION_LDS_NODE_CAP: if (v < 0) return bad(); c->lds_node_cap = v; break;

@@ -2621,6 +2621,7 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         info[RT_LI_SPARSE] = a.samples && a.sflags ? 1 : 0;
         info[RT_LI_SPAIR] = (pool && shape == LINK_LDS && a.sph_pairs && !a.box_all_cmp && a.sph_lds >= 0) ? 1 : 0;
         info[RT_LI_LEAF_PF] = (pool && (shape == LINK_LDS || shape == LINK_TL)) ? a.leaf_pf : 0;
+        info[RT_LI_WALK_FRAC] = a.walk_frac;
         info[RT_LI_SHADE_LDS] = (a.sph_mat_lds >= 0) + 2 * (a.box_mat_lds >= 0) + 4 * (a.tex_lds >= 0);
     }
     // Arguments live in device memory: the by-value kernarg struct would be copied

@@ -82,7 +82,7 @@ OPTIONS = {"box_pretest": 1, "fastdiv": 2, "sph_lds": 3, "big_wg": 4, "chunk_tar
            "tl_leaf_lds": 16, "perlin_packed": 17, "sparse_stage": 18, "sphere_pairs": 19, "leaf_prefetch": 20, "tl_small_lds": 21, "shade_lds": 22, "kernel_variant": 100, "debug_flags": 101}
 # rt_debug_last_launch fields
 LAUNCH_FIELDS = ("shape", "block", "fastdiv", "pretest", "lds_bytes", "lds_nodes", "box_records", "staged",
-                 "chunks", "spine", "sparse", "sphere_pairs", "leaf_prefetch", "shade_lds")
+                 "chunks", "spine", "sparse", "sphere_pairs", "leaf_prefetch", "shade_lds", "walk_frac")
 SHAPES = {0: "fast-lds", 1: "fast-global", 2: "link-lds", 3: "meta-lds", 4: "meta-global", 5: "link-two-level"}
 
 

@@ -162,6 +162,26 @@ def test_release_library_has_no_ab_options(gpu):
     ctx.close()
 
 
+@pytest.mark.parametrize("sid,want", [(6, 8), (0, 32), (8, 48)])
+def test_walk_threshold_by_bvh_size(gpu, sid, want):
+    """walk_frac 0 (the default) picks the walk round threshold by BVH size (rt_capi.hip
+    walk_frac_for: 8/64 up to 64 nodes, 32 up to 1024, 48 above; measured per scene); explicit
+    values override it.  Rounds only regroup lanes: the same bits at the default, 8 and 48."""
+    scene = rtamd.Scene(sid, 96, 64, seed=1)
+    imgs = []
+    for v in (0, 8, 48):
+        c = rtamd.RenderContext(options={"walk_frac": v})
+        assert c.get_option("walk_frac") == v
+        c.upload_scene(scene)
+        c.set_params(max_depth=5, spp=4096)
+        c.resize(96, 64)
+        c.render(1, rtamd.frame_rand_factors(1, 0, 6))
+        imgs.append(c.read_image())
+        assert c.last_launch()["walk_frac"] == (v or want), c.last_launch()
+        c.close()
+    assert bit_equal(imgs[0], imgs[1]) and bit_equal(imgs[0], imgs[2]), f"scene {sid}"
+
+
 def test_shading_threshold_by_kernel(gpu):
     """sm_frac 0 (the default) picks the threshold by kernel (50/64 for the compact-box kernels,
     56/64 else, rt_capi.hip); explicit values 1..64 override it and anything else is refused.
