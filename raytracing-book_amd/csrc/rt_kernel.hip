@@ -767,7 +767,9 @@ __device__ __forceinline__ uint32_t link_walk(const NodeSrc& ns, uint32_t nx, v3
 // link_walk for a wave's walking lanes that stops once `need` of them hold a hit
 // leaf or have ended (the others keep their position nx >= 0 and go on in the
 // next round): the wave does not step its last walkers alone while the lanes
-// waiting at a leaf idle.  Checked every third step (every second: scene 6 +2.7%, scenes 0 / 8 +0.6..0.8%).
+// waiting at a leaf idle.  Checked every third step (every second: scene 6 +2.7%, scenes 0 / 8 +0.6..0.8%;
+// round 4, under the per-BVH walk thresholds, every 2nd / 4th: scenes 6 / 7 +9..15%, 0 / 8 -0.1..+1.2%,
+// profiles/r04_walk_check_interval_lib_ab.log).
 template <bool EXACT, bool STATS, bool TL = false>
 __device__ __forceinline__ uint32_t link_walk_part(const NodeSrc& ns, uint32_t nx, v3 o, v3 inv, float tmin,
                                                    float tmax, int need, unsigned long long* st) {
