@@ -422,7 +422,8 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
 // many 64ths of its lanes hold a leaf or ended.  Measured per scene (round 4,
 // profiles/r04_knobs*_s*.log; the default was 48 for every scene): the 7-node Cornell boxes
 // want short rounds (scene 6: 8..16 -6%, scene 7: 8 -8.6%, 16 -2.5%), scene 0's 511 nodes 32..36
-// (-1.3%), scene 8's 1793 nodes 48..52 (44: +0.4%).  Rounds only regroup which lanes walk and
+// (-1.3%), scene 8's 1793 nodes 48..52 (44: +0.4%); a two-level launch takes 32 (LDS plan below).
+// Rounds only regroup which lanes walk and
 // test leaves together: every lane's node and prim sequence is unchanged (bit-identical).
 int walk_frac_for(int n_nodes) { return n_nodes <= 64 ? 8 : n_nodes <= 1024 ? 32 : 48; }
 
@@ -1689,6 +1690,10 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             cap = tl ? cap_b : cap_s;
         }
         a.block = cap == cap_b ? 1024 : 512;
+        // the two-level walk's rounds: 32 (its walks wait on global nodes; 16 / 24 / 32 / 48 / 64 on
+        // the 4000-sphere cloud at a 32 KB cap and the 9000-sphere cloud: 32 best, -1.7% against 48,
+        // profiles/r04_bvh_walk_frac_*.log)
+        if (tl && !c->walk_frac) a.walk_frac = 32;
         size_t at = 0;
         a.lds_node_f4 = 0;
         a.leaf_lds = -1;

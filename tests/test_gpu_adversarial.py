@@ -96,6 +96,7 @@ def test_two_level_walk_forced(gpu, cap, tll, small):
     ref = oracle(case)
     out, info = render(case, {"lds_node_cap": cap, "tl_leaf_lds": tll, "tl_small_lds": small})
     assert info["shape_name"] == "link-two-level" and info["lds_nodes"] == cap // 32, info
+    assert info["walk_frac"] == 32, info   # the two-level rounds (rt_capi.hip LDS plan)
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
