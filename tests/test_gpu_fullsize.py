@@ -154,14 +154,14 @@ def test_lds_record_copies_change_no_bit_1080p(gpu, knob, sid):
 # every non-default walk or scheduling form is gated here, bit for bit).
 WALK_OPTIONS = [
     ("sm_frac", {"sm_frac": 8}), ("sm_frac", {"sm_frac": 64}), ("sm_batch", {"sm_batch": 16}),
-    ("walk_frac", {"walk_frac": 16}), ("walk_frac", {"walk_frac": 64}),
+    ("walk_frac", {"walk_frac": 16}), ("walk_frac", {"walk_frac": 48}), ("walk_frac", {"walk_frac": 64}),
     ("sphere_pairs", {"sphere_pairs": 0}), ("spine", {"spine": 0}), ("leaf_prefetch", {"leaf_prefetch": 0}),
     ("shade_lds", {"shade_lds": 0}),
     ("two_level", {"lds_node_cap": 16384}), ("two_level_leaf_global", {"lds_node_cap": 16384, "tl_leaf_lds": 0}),
 ]
 
 
-@pytest.mark.parametrize("sid", [8, 0])
+@pytest.mark.parametrize("sid", [8, 0, 6])
 @pytest.mark.parametrize("name,opts", WALK_OPTIONS, ids=[f"{n}-{list(o.values())[-1]}" for n, o in WALK_OPTIONS])
 def test_walk_and_schedule_options_change_no_bit_1080p(gpu, sid, name, opts):
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
