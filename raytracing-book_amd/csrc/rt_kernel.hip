@@ -2181,7 +2181,11 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             inv = mk3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
             a = g_dot(S.d, S.d);
         }
-        // rounds of node walk + leaf tests (trace())
+        // rounds of node walk + leaf tests (trace()), at wave priority 1: their dependent LDS
+        // chains then issue as soon as their data is back, and the shading's long VALU runs (at
+        // priority 0) fill the gaps -- scene 8 -3.1%, scene 0 -2.1%, scenes 6 / 7 -0.4 / -1.2%
+        // (profiles/r04_setprio_combined_lib_ab.log; the walk alone at 1: scene 6 +0.6%)
+        __builtin_amdgcn_s_setprio(1);
         for (;;) {
             const unsigned long long tr = __ballot(status == RT_SM_TRACE);
             const int n_hit = __popcll(__ballot(status == RT_SM_HIT));
@@ -2220,6 +2224,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                 }
             }
         }
+        __builtin_amdgcn_s_setprio(0);
         // shade the HIT lanes together
         if (status == RT_SM_HIT) {
             unsigned long long ts = STATS ? clock64() : 0;
