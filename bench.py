@@ -26,8 +26,11 @@ The rank-0 JSON line carries
     tools/valu_peak.hip measures the 4-waves-per-SIMD ceiling, also reported);
   * cpu_baseline: the CPU oracle (oracle/, a restatement of the reference's
     GLSL; the reference has no CPU path) with one thread per CPU of the job's
-    cgroup quota (else its affinity set), >= 60 s, on a bounded stripe of the
-    same workload, plus its single-thread rate and the C1 CPU config in full.
+    cgroup quota (else its affinity set), 30 s unpinned and 30 s with each thread
+    pinned to its own physical core, on a bounded stripe of the same workload,
+    plus its single-thread rate, the load average and the C1 CPU config in full;
+  * gather_parity (N > 1): rank 0 re-renders each rank's first stripe alone and
+    compares it bit for bit with the gathered image.
 """
 import argparse
 import json
@@ -130,6 +133,28 @@ def cpu_threads(facts):
     return max(1, int(n))
 
 
+def physical_core_cpus(cpus):
+    """One logical CPU per physical core of `cpus` (the lowest id of each SMT sibling set,
+    /sys/devices/system/cpu/cpu*/topology/thread_siblings_list), in id order."""
+    cpus = sorted(set(cpus))
+    seen, out = set(), []
+    for c in cpus:
+        try:
+            txt = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+            sib = set()
+            for part in txt.split(","):
+                lo, _, hi = part.partition("-")
+                sib.update(range(int(lo), int(hi or lo) + 1))
+        except (OSError, ValueError):
+            sib = {c}
+        key = min(sib)
+        if key in seen:
+            continue
+        seen.add(key)
+        out.append(min(sib & set(cpus)) if sib & set(cpus) else c)
+    return out
+
+
 def _oracle_rate(pyoracle, rtamd, osc, W, H, rows_rank, rows_world, stripe, seed, seconds, threads):
     """Frames of the rows of one stripe set, in growing chunks, until `seconds`."""
     image = np.zeros((H, W, 4), np.float32)
@@ -149,44 +174,75 @@ def _oracle_rate(pyoracle, rtamd, osc, W, H, rows_rank, rows_world, stripe, seed
 def cpu_baseline(scene, args):
     """CPU oracle (oracle/, the build's scalar restatement of compute.glsl; the
     reference has no CPU path) on this host.  One thread per usable
-    CPU (cpu_threads), >= args.cpu_seconds on the full-width rows of stripe 0 of 8 of the same
-    workload; the rate does not depend on spp.  Also: a 1-thread rate, the C1
-    config (scene 9, 400x225, 64 spp, depth 8) rendered in full, and the host
-    facts (the job's cgroup CPU quota caps what many threads can get)."""
+    CPU (cpu_threads) on the full-width rows of stripe 0 of 8 of the same workload
+    (the rate does not depend on spp), twice: threads left to the scheduler, and
+    each thread pinned to its own physical core of the affinity set (one CPU per SMT
+    pair); `value` is the better of the two.  Also: a 1-thread
+    rate (pinned) on the same rows, the load average before and after, the C1 config
+    (scene 9, 400x225, 64 spp, depth 8) rendered in full, and the host facts."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     import rtamd
     facts = host_facts()
     threads = cpu_threads(facts)
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
+    cores = physical_core_cpus(aff)
+    pin = cores[:threads] if len(cores) >= threads else cores + [c for c in aff if c not in cores][:threads - len(cores)]
+    load0 = os.getloadavg()
     osc = pyoracle.OracleScene(scene, max_depth=args.depth, spp=args.spp_total)
     W, H = scene.width, scene.height
-    samples, nf, rows, dt = _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 8, args.stripe_rows, args.seed,
-                                         args.cpu_seconds, threads)
-    # one thread on the same rows (stripe 0 of 8), so that the two rates compare like for like
-    s1, nf1, rows1, dt1 = _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 8, args.stripe_rows, args.seed,
-                                       min(15.0, args.cpu_seconds), 1)
-    # C1 (BASELINE.json configs[0]): the CPU reference path's own config, in full
+    half = max(5.0, args.cpu_seconds / 2)
+
+    def run(cpus, nthreads, seconds):
+        pyoracle.set_thread_cpus(cpus)
+        try:
+            return _oracle_rate(pyoracle, rtamd, osc, W, H, 0, 8, args.stripe_rows, args.seed, seconds, nthreads)
+        finally:
+            pyoracle.set_thread_cpus(None)
+
+    s_u, nf_u, rows, dt_u = run(None, threads, half)
+    s_p, nf_p, _, dt_p = run(pin, threads, half)
+    # one thread on the same rows (stripe 0 of 8), pinned, so that the rates compare like for like
+    s1, nf1, rows1, dt1 = run(pin[:1], 1, min(15.0, args.cpu_seconds))
+    load1 = os.getloadavg()
+    # C1 (BASELINE.json configs[0]): the CPU reference path's own config, in full (pinned)
     c1 = rtamd.Scene(9, 400, 225, seed=args.seed)
     oc1 = pyoracle.OracleScene(c1, max_depth=8, spp=64)
     rf = rtamd.frame_rand_factors(args.seed, 0, 64)
+    pyoracle.set_thread_cpus(pin)
     t = time.perf_counter()
     pyoracle.render(oc1, rf, first_frame=1, nthreads=threads)
     c1_s = time.perf_counter() - t
+    pyoracle.set_thread_cpus(None)
     per_thread = s1 / dt1 / 1e6
+    r_u, r_p = s_u / dt_u / 1e6, s_p / dt_p / 1e6
+    best_pinned = r_p >= r_u
+    samples, nf, dt = (s_p, nf_p, dt_p) if best_pinned else (s_u, nf_u, dt_u)
     return {
-        "value": round(samples / dt / 1e6, 3),
+        "value": round(max(r_u, r_p), 3),
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
         "threads": threads,
         "threads_rule": "round(cgroup CPU quota), else the affinity CPU count, capped by both",
+        "pinning": "pinned" if best_pinned else "unpinned",
         **facts,
         "sample": f"scene {args.scene} {W}x{H} max_depth {args.depth}: rows of stripe 0/8 ({rows} rows x {W}), "
-                  f"{nf} frames = {samples} samples in {dt:.1f} s, {threads} threads",
+                  f"{nf} frames = {samples} samples in {dt:.1f} s, {threads} threads "
+                  f"({'one per physical core, pinned' if best_pinned else 'unpinned'})",
+        "unpinned_msamples_s": round(r_u, 3),
+        "pinned_msamples_s": round(r_p, 3),
+        "pinned_cpus": pin,
+        "physical_cores_in_affinity": len(cores),
         "single_thread_msamples_s": round(per_thread, 3),
-        "single_thread_sample": f"the same rows, {nf1} frames = {s1} samples in {dt1:.1f} s, 1 thread",
+        "single_thread_sample": f"the same rows, {nf1} frames = {s1} samples in {dt1:.1f} s, 1 thread pinned "
+                                f"to CPU {pin[0] if pin else '?'}",
         "single_thread_x_threads_msamples_s": round(per_thread * threads, 3),
-        "parallel_efficiency": round(samples / dt / 1e6 / (per_thread * threads), 3),
+        "parallel_efficiency": round(max(r_u, r_p) / (per_thread * threads), 3),
+        "parallel_efficiency_unpinned": round(r_u / (per_thread * threads), 3),
+        "parallel_efficiency_pinned": round(r_p / (per_thread * threads), 3),
+        "loadavg_start": [round(x, 2) for x in load0],
+        "loadavg_end": [round(x, 2) for x in load1],
         "extrapolated_not_measured": {
             "physical_cores_x_single_thread_msamples_s": round(per_thread * facts["physical_cores"], 1)
             if facts["physical_cores"] else None,
@@ -194,8 +250,39 @@ def cpu_baseline(scene, args):
                     "job's CPU quota, not a measurement"},
         "c1": {"config": "scene 9 (Book-1 three spheres), 400x225, 64 spp, max_depth 8, full render",
                "samples": 400 * 225 * 64, "seconds": round(c1_s, 3),
-               "msamples_s": round(400 * 225 * 64 / c1_s / 1e6, 3), "threads": threads},
+               "msamples_s": round(400 * 225 * 64 / c1_s / 1e6, 3), "threads": threads, "pinned": True},
     }
+
+
+# ---------------------------------------------------------------- gather parity
+def gather_parity(scene, args, full, world, dev, factors, n_frames):
+    """the gathered image checked bit for bit, on rank 0 after the timed
+    region.  For every rank k, the first stripe it owns (stripe k, rows [8k, 8k+8)) is
+    re-rendered alone -- a 1-device context partitioned as rank k of one rank per stripe,
+    so it owns stripe k only -- over the same frames and rand factors, and compared with
+    those rows of `full`.  A stripe block received at a wrong offset, a wrong rank's block
+    or a wrong de-interleave shows up here; nan_pixels cannot catch it.  Any row partition
+    renders the same bits as one GPU (tests/test_gpu_fullsize.py), so a match is exact."""
+    import rtamd
+    H, W, sr = args.height, args.width, args.stripe_rows
+    n_stripes = (H + sr - 1) // sr
+    ok, checked = True, []
+    for k in range(min(world, n_stripes)):
+        c = rtamd.RenderContext(devices=(dev,), rank=k, world=n_stripes, stripe_rows=sr)
+        try:
+            c.upload_scene(scene)
+            c.set_params(max_depth=args.depth, spp=args.spp_total)
+            c.resize(W, H)
+            c.render(1, factors[:n_frames])
+            blk = c.read_image()
+        finally:
+            c.close()
+        ref = full[k * sr:min(H, (k + 1) * sr)]
+        same = blk.shape == ref.shape and np.array_equal(np.isnan(blk), np.isnan(ref)) and \
+            np.array_equal(blk.view(np.uint32)[~np.isnan(blk)], ref.view(np.uint32)[~np.isnan(ref)])
+        ok = ok and bool(same)
+        checked.append(k)
+    return ok, checked
 
 
 # ---------------------------------------------------------------- roofline
@@ -353,6 +440,12 @@ def main():
     if args.png:
         rtamd.save_png(full, args.png)
     nan_px = int(np.isnan(full[..., :3]).any(axis=-1).sum())
+    g_ok, g_stripes = None, []
+    if world > 1:   # other ranks wait in the final barrier meanwhile
+        try:
+            g_ok, g_stripes = gather_parity(scene, args, full, world, dev, factors, F * total_steps)
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            log("gather parity check failed to run:", repr(e))
 
     cpu = None
     # the CPU baseline is an N = 1 figure (rank 0 of a one-GPU run); an N-rank run skips it so
@@ -389,6 +482,8 @@ def main():
         "gather_ms": round(gather_ms, 3),
         "gather_path": gather_path,
         "gather_native_error": gather_err,
+        "gather_parity": g_ok,
+        "gather_parity_stripes": len(g_stripes),
         "nan_pixels": nan_px,
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -55,6 +55,8 @@ def lib():
         L.oracle_render.argtypes = [ctypes.POINTER(OracleSceneDesc), ctypes.c_int, ctypes.c_int, fp, ctypes.c_int,
                                     ctypes.c_int, fp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(OracleCounters)]
+        L.oracle_set_thread_cpus.restype = None
+        L.oracle_set_thread_cpus.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.oracle_get_sphere_uv.argtypes = [ctypes.c_float] * 3 + [fp, fp]
         L.oracle_rand_sequence.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_int, fp]
         L.oracle_eval_builtin.argtypes = [ctypes.c_int, fp, fp, fp, ctypes.c_int]
@@ -122,6 +124,13 @@ def render(oscene, rand_factors, first_frame=1, image=None, rank=0, world=1, str
     if counters:
         return image, {n: getattr(cnt, n) for n in COUNTER_FIELDS}
     return image
+
+
+def set_thread_cpus(cpus):
+    """Pin render()'s worker i to CPU cpus[i % len(cpus)]; None or [] unpins."""
+    cpus = list(cpus or [])
+    arr = (ctypes.c_int * max(1, len(cpus)))(*cpus)
+    lib().oracle_set_thread_cpus(arr, len(cpus))
 
 
 def sphere_uv(x, y, z):

@@ -19,8 +19,12 @@
 #include "rt/rt_glsl.h"
 #include "rt/rt_types.h"
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <atomic>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -780,9 +784,18 @@ bool make_scene(const oracle_scene_desc* d, Scene& S) {
     return true;
 }
 
+// CPUs the render threads are pinned to (empty: not pinned); bench.py's baseline only
+std::mutex g_pin_mu;
+std::vector<int> g_pin;
+
 }  // namespace
 
 extern "C" {
+
+void oracle_set_thread_cpus(const int* cpus, int n) {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pin.assign(cpus && n > 0 ? cpus : nullptr, cpus && n > 0 ? cpus + n : nullptr);
+}
 
 int oracle_render(const oracle_scene_desc* d, int width, int height, float* rgba, int first_frame, int n_frames,
                   const float* rand_factors, int rank, int world, int stripe_rows, int nthreads,
@@ -813,10 +826,32 @@ int oracle_render(const oracle_scene_desc* d, int width, int height, float* rgba
             }
         }
     };
+    // optional pinning (oracle_set_thread_cpus): worker i runs on CPU g_pin[i % n], the
+    // calling thread's own mask restored afterwards
+    std::vector<int> pin;
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        pin = g_pin;
+    }
+    cpu_set_t saved;
+    const bool pinned = !pin.empty() && sched_getaffinity(0, sizeof(saved), &saved) == 0;
+    auto pin_self = [&](int i) {
+        if (!pinned) return;
+        cpu_set_t s;
+        CPU_ZERO(&s);
+        CPU_SET(pin[(size_t)i % pin.size()], &s);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof(s), &s);
+    };
     std::vector<std::thread> th;
-    for (int i = 1; i < nthreads; i++) th.emplace_back(worker, i);
+    for (int i = 1; i < nthreads; i++)
+        th.emplace_back([&, i]() {
+            pin_self(i);
+            worker(i);
+        });
+    pin_self(0);
     worker(0);
     for (auto& t : th) t.join();
+    if (pinned) (void)pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
     if (counters) {
         std::memset(counters, 0, sizeof(*counters));
         for (auto& p : per) {

@@ -61,6 +61,10 @@ int oracle_render(const oracle_scene_desc* d, int width, int height, float* rgba
                   int rank, int world, int stripe_rows, int nthreads,
                   oracle_counters* counters);
 
+/* Pin oracle_render's threads: worker i to CPU cpus[i % n] (n = 0: unpinned, the
+ * default).  Used by bench.py's CPU baseline only. */
+void oracle_set_thread_cpus(const int* cpus, int n);
+
 /* Analysis hook: per-trace BVH node sequences for a pixel window
  * (records [pixel, frame, bounce, n, node...]); returns int32 count. */
 long oracle_trace_log(const oracle_scene_desc* d, int width, int height, int x0, int x1, int y0, int y1,

@@ -57,11 +57,28 @@ def gather_image(local_block, height, world, stripe_rows):
     return None
 
 
+def _agree(ok, what):
+    """Every rank learns whether every rank got through `what` (MIN all-reduce): a failure on
+    one rank raises on all of them, so none is left blocked in the next RCCL call."""
+    dev = "cpu"
+    if dist.get_backend() == "nccl":
+        dev = f"cuda:{torch.cuda.current_device()}"
+    t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if float(t.item()) < 1.0:
+        raise RuntimeError(f"native gather: {what} failed on some rank")
+
+
 def native_gather(ctx, rank, world):
     """The gather through the C ABI (rt_comm_init + rt_gather_image: RCCL sends to rank 0,
     de-interleave kernel there): rank 0 makes the communicator id, torch.distributed
-    hands it to the other ranks (the only use of torch.distributed here).  Returns the
-    [H, W, 4] image on rank 0, None elsewhere."""
+    hands it to the other ranks and agrees, between the steps, that every rank got
+    through the last one.  Returns the [H, W, 4] image on rank 0, None elsewhere.
+
+    The agreements bound what one rank's failure can do to the others:
+    rt_comm_init's argument checks are made on every rank before any rank enters
+    ncclCommInitRank (a collective), and every rank's render is synchronised (rt_sync,
+    which reports a device fault) before any rank enters the Send / Recv group."""
     from . import render
     if world == 1:
         return ctx.read_image()
@@ -78,5 +95,19 @@ def native_gather(ctx, rank, world):
     uid, err = box[0]
     if uid is None:
         raise RuntimeError(f"rank 0 could not make an RCCL communicator id: {err}")
-    ctx.comm_init(uid, rank, world)
+    # rt_comm_init's own preconditions (rt_capi.hip: a 1-device context partitioned as (rank, world))
+    _agree(len(getattr(ctx, "devices", (0,))) == 1 and getattr(ctx, "rank", rank) == rank
+           and getattr(ctx, "world", world) == world, "the rt_comm_init preconditions")
+    ok = True
+    try:
+        ctx.comm_init(uid, rank, world)
+    except Exception:  # noqa: BLE001 -- every rank raises in _agree
+        ok = False
+    _agree(ok, "rt_comm_init")
+    ok = True
+    try:
+        ctx.sync()
+    except Exception:  # noqa: BLE001
+        ok = False
+    _agree(ok, "rt_sync before the gather")
     return ctx.gather_image()

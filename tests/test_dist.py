@@ -76,8 +76,12 @@ def test_gloo_stripe_gather(world):
 class _FakeCtx:
     """Stands in for rtamd.RenderContext in the native gather's host logic (no GPU here)."""
 
-    def __init__(self, rank, image=None):
+    def __init__(self, rank, image=None, world=2, fail_init=False):
         self.rank, self.image, self.uid, self.calls = rank, image, None, []
+        self.world, self.devices, self.fail_init = world, (0,), fail_init
+
+    def sync(self):
+        self.calls.append("sync")
 
     def read_image(self):
         self.calls.append("read_image")
@@ -85,6 +89,8 @@ class _FakeCtx:
 
     def comm_init(self, uid, rank, world):
         self.calls.append(("comm_init", rank, world))
+        if self.fail_init:
+            raise OSError("rt_comm_init: ncclCommInitRank failed")
         self.uid = bytes(uid)
 
     def gather_image(self):
@@ -95,12 +101,12 @@ class _FakeCtx:
 def test_native_gather_world1_is_read_image():
     """at world 1 the C-ABI gather (bench.py's gather path) is rt_read_image."""
     img = np.random.default_rng(1).random((7, 5, 4), dtype=np.float32)
-    c = _FakeCtx(0, img)
+    c = _FakeCtx(0, img, world=1)
     out = rdist.native_gather(c, 0, 1)
     assert out is img and c.calls == ["read_image"]
 
 
-def _native_worker(rank, world, port, q, fail=False):
+def _native_worker(rank, world, port, q, fail=False, fail_init_rank=None):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         rdist.init_from_env(backend="gloo")
@@ -112,7 +118,8 @@ def _native_worker(rank, world, port, q, fail=False):
                 raise OSError("librccl.so.1: cannot open shared object file")
             return bytes(range(7, 7 + 128))
         R.comm_unique_id = fake_uid
-        c = _FakeCtx(rank, np.full((3, 2, 4), 5.0, np.float32) if rank == 0 else None)
+        c = _FakeCtx(rank, np.full((3, 2, 4), 5.0, np.float32) if rank == 0 else None, world=world,
+                     fail_init=rank == fail_init_rank)
         try:
             out = rdist.native_gather(c, rank, world)
             q.put((rank, c.uid, c.calls, None if out is None else out.shape))
@@ -148,7 +155,7 @@ def test_native_gather_hands_rank0_id_to_every_rank():
     uid = bytes(range(7, 7 + 128))
     for r in range(world):
         _, got, calls, shape = by_rank[r]
-        assert got == uid and calls == [("comm_init", r, world), "gather_image"], (r, calls)
+        assert got == uid and calls == [("comm_init", r, world), "sync", "gather_image"], (r, calls)
         assert shape == ((3, 2, 4) if r == 0 else None)
 
 
@@ -175,6 +182,30 @@ def test_native_gather_id_failure_raises_on_every_rank():
         assert m[1] == "raised" and m[2] == [] and "cannot open" in m[3], m
 
 
+def test_native_gather_one_rank_comm_init_failure_raises_on_every_rank():
+    """if only rank 1 fails in rt_comm_init, rank 0 must not go on into rt_gather_image
+    (its Recv would wait for a Send that never comes): every rank raises, none calls gather_image,
+    and bench.py falls back to the torch gather on all ranks."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_worker, args=(r, world, port, q, False, 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    msgs = []
+    while not q.empty():
+        msgs.append(q.get())
+    assert sorted(m[0] for m in msgs) == [0, 1], msgs
+    for m in msgs:
+        assert m[1] == "raised" and "gather_image" not in m[2] and "rt_comm_init" in m[3], m
+
+
 def test_bench_cpu_threads_follow_the_quota():
     """the CPU baseline uses the job's CPUs (cgroup quota, else affinity), not nproc."""
     import importlib.util
@@ -186,6 +217,9 @@ def test_bench_cpu_threads_follow_the_quota():
     assert bench.cpu_threads({"nproc": 256, "affinity_cpus": 8, "cgroup_cpu_quota": 16.0}) == 8
     assert bench.cpu_threads({"nproc": 256, "affinity_cpus": 12, "cgroup_cpu_quota": None}) == 12
     assert bench.cpu_threads({"nproc": 4, "affinity_cpus": 4, "cgroup_cpu_quota": 0.4}) == 1
+    # one CPU per physical core of the affinity set for the pinned run
+    cores = bench.physical_core_cpus(sorted(os.sched_getaffinity(0)))
+    assert cores and len(set(cores)) == len(cores) and set(cores) <= set(os.sched_getaffinity(0))
 
 
 def test_gather_single_rank_is_identity():
