@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=60.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--png", default=None)
+    p.add_argument("--fast-bvh", action="store_true",
+                   help="the non-parity fast mode (rt_set_bvh_mode RT_BVH_SAH): a separate line, never the headline")
     a = p.parse_args()
     pre = PRESETS[a.preset]
     for k in ("scene", "width", "height", "spp_total"):
@@ -91,7 +93,32 @@ def parse():
 
 
 def config_key(a, frames):
-    return f"scene{a.scene}_{a.width}x{a.height}_f{frames}_d{a.depth}"
+    return f"scene{a.scene}_{a.width}x{a.height}_f{frames}_d{a.depth}" + ("_sah" if a.fast_bvh else "")
+
+
+def bvh_counts(scene, args):
+    """Node visits and prim tests per sample of the reference BVH and of the SAH tree, from the
+    oracle's counters (the reference's stack walk over each tree) on a small render of the same
+    scene (240x135, 8 frames): what the fast mode removes."""
+    import types
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    import rtamd
+    sc = rtamd.Scene(args.scene, 240, 135, seed=args.seed)
+    rf = rtamd.frame_rand_factors(args.seed, 0, 8)
+    out = {"sample": "oracle counters, 240x135, 8 frames, the same scene and depth"}
+    for name, b in (("reference", sc.buffers[1]), ("sah", rtamd.sah_bvh(sc))):
+        v = types.SimpleNamespace(**{k: getattr(sc, k) for k in ("textures", "camera", "background", "width",
+                                                                 "height")})
+        v.buffers = dict(sc.buffers)
+        v.buffers[1] = b
+        _, c = pyoracle.render(pyoracle.OracleScene(v, max_depth=args.depth, spp=args.spp_total), rf,
+                               nthreads=min(16, os.cpu_count() or 1), counters=True)
+        n = c["samples"]
+        out[name] = {"bvh_nodes": len(b) // 32, "node_visits_per_sample": round(c["node_visits"] / n, 2),
+                     "prim_tests_per_sample": round((c["sphere_tests"] + c["box_tests"] + c["quad_tests"] +
+                                                     c["medium_tests"]) / n, 2)}
+    return out
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -346,6 +373,8 @@ def main():
 
     scene = rtamd.Scene(args.scene, args.width, args.height, seed=args.seed)
     ctx = rtamd.RenderContext(devices=(dev,), rank=rank, world=world, stripe_rows=args.stripe_rows)
+    if args.fast_bvh:
+        ctx.set_bvh_mode("sah")
     ctx.upload_scene(scene)
     ctx.set_params(max_depth=args.depth, spp=args.spp_total)
     ctx.resize(args.width, args.height)
@@ -441,7 +470,7 @@ def main():
         rtamd.save_png(full, args.png)
     nan_px = int(np.isnan(full[..., :3]).any(axis=-1).sum())
     g_ok, g_stripes = None, []
-    if world > 1:   # other ranks wait in the final barrier meanwhile
+    if world > 1 and not args.fast_bvh:   # other ranks wait in the final barrier meanwhile
         try:
             g_ok, g_stripes = gather_parity(scene, args, full, world, dev, factors, F * total_steps)
         except Exception as e:  # noqa: BLE001 -- reported, never fatal
@@ -460,8 +489,19 @@ def main():
     samples_per_launch = n_local_px * frames_per_launch
     roof = roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms)
 
+    fast = None
+    if args.fast_bvh:
+        fast = {"mode": "RT_BVH_SAH (rt_set_bvh_mode): non-parity fast mode, NOT the headline",
+                "parity": "statistical against the reference BVH (tests/test_gpu_fast_bvh.py, the gallery anchors); "
+                          "bit-exact against the oracle walking the same SAH tree",
+                "bvh_mode_ran": ctx.last_launch()["bvh_mode"]}
+        try:
+            fast["bvh_counts"] = bvh_counts(scene, args)
+        except Exception as e:  # noqa: BLE001 -- reported
+            fast["bvh_counts_error"] = repr(e)
+
     out = {
-        "metric": METRIC,
+        "metric": METRIC + (" [fast mode: SAH BVH, non-parity]" if args.fast_bvh else ""),
         "value": round(value, 2),
         "unit": "Msamples/s",
         "n_gpus": world,
@@ -488,6 +528,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
     }
+    if fast:
+        out["fast_bvh"] = fast
     print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.barrier()

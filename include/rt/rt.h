@@ -154,6 +154,18 @@ int rt_gather_path(rt_ctx* ctx);
 int rt_deinterleave_rows(const float* gathered, int width, int height, int world,
                          int stripe_rows, float* rgba_out);
 
+/* ---- Non-parity fast mode -------------------------------
+ * RT_BVH_REFERENCE (default): the walk runs on the uploaded BVH -- the reference's median
+ * split (BVHNode.java:13-56) -- and every image is bit-identical to the reference semantics.
+ * RT_BVH_SAH: the context rebuilds the BVH from the uploaded BVH's prims with a binned-SAH
+ * builder (leaves of at most two prims; each medium keeps its reference leaf, so its test
+ * multiplicity and hence its density are the reference's) and walks that.  Same kernel, same
+ * leaf tests; far fewer node visits and prim tests.  NOT bit-exact against the reference
+ * BVH: a medium's rand() draws fall at another point of the visit sequence, so images agree
+ * statistically (tests/test_gpu_fast_bvh.py).  Takes effect at the next rt_render. */
+enum { RT_BVH_REFERENCE = 0, RT_BVH_SAH = 1 };
+int rt_set_bvh_mode(rt_ctx* ctx, int mode);
+
 /* Per-frame u_rand_factor for frame index f (0-based) of a seeded render:
  * top 24 bits of splitmix64(seed, f) / 2^24, in [0,1).  Stands in for the
  * reference's (float)Math.random() per frame (RaytraceExecutor.java:124). */

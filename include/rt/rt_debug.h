@@ -109,9 +109,10 @@ enum {
     RT_OPTION_LEAF_PREFETCH = 20,       /* compact-box kernels: each leaf slot's record loaded
                                            before the prim-type blocks when spheres, boxes
                                            and media are all staged in LDS (1)              */
-    RT_OPTION_TL_SMALL_LDS = 21,        /* two-level walk: the sphere / compact box records
-                                           staged beside the top levels when each takes at
-                                           most 1/16 of the room (1)                        */
+    RT_OPTION_TL_SMALL_LDS = 21,        /* two-level walk: room is reserved beside the top
+                                           levels for the sphere / compact box records that
+                                           take at most 1/16 of it, and each table is staged
+                                           whenever it fits after the nodes (1); 0: neither */
     RT_OPTION_SHADE_LDS = 22,           /* shading tables in LDS: sphere and compact box
                                            materials, texture descriptors, small texture
                                            slots (1)                                        */
@@ -132,8 +133,27 @@ int rt_debug_get_option(struct rt_ctx* ctx, int option, int* value);
  *   out[9] spine nodes a walk may skip (0 = off)
  *   out[10] sparse staging (1 = a flag byte per sample, only non-zero colours stored)
  *   out[11] sphere-pair kernel (1 = a two-sphere leaf's spheres tested at once)
+ *   out[12] leaf record prefetch  out[13] shading tables in LDS (bits)  out[14] walk threshold
+ *   out[15] the BVH the walk ran on: RT_BVH_REFERENCE (0) or RT_BVH_SAH (1, rt_set_bvh_mode)
  * n <= 16 ints are written; returns RT_ERR_STATE before the first render. */
 int rt_debug_last_launch(struct rt_ctx* ctx, int* out, int n);
+
+/* The BVH the link walk of ctx uses, in the reference's node format (rt_bvh_node): the
+ * uploaded one, or in RT_BVH_SAH mode the tree rt_set_bvh_mode builds (validated as by
+ * rt_render).  out may be NULL to query *nbytes; returns RT_ERR_LIMIT if out_cap is short.
+ * Tests feed it to the CPU oracle: the kernel on the SAH tree is bit-exact against the
+ * oracle walking the same tree. */
+int rt_debug_walk_bvh(struct rt_ctx* ctx, void* out, size_t out_cap, size_t* nbytes);
+
+/* Context-free form of the RT_BVH_SAH build (no device needed): the SAH tree over the prims
+ * of `bvh` (the reference's nodes), from the uploaded record bytes of the other bindings.
+ * order: 0 the larger child (surface area) first, 1 the smaller first, 2 the child nearer
+ * to eye[3] first (rt_set_bvh_mode's, with the camera position); prim_cost: the SAH cost of a
+ * prim test in node steps (rt_set_bvh_mode's: 1). */
+int rt_debug_build_sah_bvh(const void* spheres, size_t sph_bytes, const void* quads, size_t quad_bytes,
+                           const void* media, size_t med_bytes, const void* boxes, size_t box_bytes,
+                           const void* bvh, size_t bvh_bytes, int order, const float eye[3],
+                           float prim_cost, void* out, size_t out_cap, size_t* nbytes);
 
 #ifdef __cplusplus
 }

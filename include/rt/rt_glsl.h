@@ -103,11 +103,17 @@ RT_HD float g_length(v3 a) { return sqrtf(g_dot(a, a)); }
  * 1/sqrt(x): +-0 -> +-inf, +inf -> +0, x < 0 and NaN -> NaN.  About a dozen operations where
  * the IEEE 1/sqrtf(x) takes two correctly rounded operations of ~13 each on gfx950. */
 RT_HD float g_inversesqrt(float x) {
-    float y = rt_u2f(0x5f375a86u - (rt_f2u(x) >> 1));
-    const float h = 0.5f * x;
+    /* a subnormal x is scaled by 2^24 first (exact) and the result by 2^12: the bit-level guess
+     * is far off below FLT_MIN, where three Newton steps would not converge; normal
+     * inputs take the same operations as before (scale 1) */
+    const int sub = x < 1.17549435e-38f;
+    const float xs = sub ? x * 16777216.0f : x;
+    float y = rt_u2f(0x5f375a86u - (rt_f2u(xs) >> 1));
+    const float h = 0.5f * xs;
     y = fmaf(y, fmaf(-h, y * y, 0.5f), y);
     y = fmaf(y, fmaf(-h, y * y, 0.5f), y);
     y = fmaf(y, fmaf(-h, y * y, 0.5f), y);
+    y = y * (sub ? 4096.0f : 1.0f);
     if (x == 0.0f) y = rt_u2f(rt_f2u(x) | 0x7f800000u);   /* +-inf with x's sign */
     if (x == __builtin_inff()) y = 0.0f;
     if (!(x >= 0.0f)) y = __builtin_nanf("");              /* x < 0 or NaN (-0 passes: -inf above) */

@@ -24,6 +24,7 @@
 #include "rt/rt_debug.h"
 #include "rt/rt_types.h"
 #include "rt_device.h"
+#include "bvh_sah.h"
 
 namespace {
 
@@ -36,6 +37,7 @@ struct Rccl {
     decltype(&ncclCommInitRank) CommInitRank = nullptr;
     decltype(&ncclCommInitAll) CommInitAll = nullptr;
     decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclCommAbort) CommAbort = nullptr;   // optional: an error inside a group aborts
     decltype(&ncclSend) Send = nullptr;
     decltype(&ncclRecv) Recv = nullptr;
     decltype(&ncclGroupStart) GroupStart = nullptr;
@@ -51,7 +53,7 @@ Rccl& rccl() {
         if (r.h) {
 #define RT_SYM(F) r.F = reinterpret_cast<decltype(r.F)>(dlsym(r.h, "nccl" #F))
             RT_SYM(GetUniqueId); RT_SYM(CommInitRank); RT_SYM(CommInitAll); RT_SYM(CommDestroy); RT_SYM(Send);
-            RT_SYM(Recv); RT_SYM(GroupStart); RT_SYM(GroupEnd); RT_SYM(GetErrorString);
+            RT_SYM(Recv); RT_SYM(GroupStart); RT_SYM(GroupEnd); RT_SYM(GetErrorString); RT_SYM(CommAbort);
 #undef RT_SYM
             r.ok = r.GetUniqueId && r.CommInitRank && r.CommInitAll && r.CommDestroy && r.Send && r.Recv &&
                    r.GroupStart && r.GroupEnd && r.GetErrorString;
@@ -134,6 +136,11 @@ struct rt_ctx {
     int proc_rank = 0, proc_world = 1, stripe_rows = 16;
     int n_dnodes = 0;
     std::vector<rt_dnode> dnodes;   // host copy of the threaded BVH (fast-walk tables are built from it)
+    // the BVH the link walk runs on (rt_set_bvh_mode): the uploaded one (RT_BVH_REFERENCE), or the
+    // binned-SAH tree built from its prims at validation (RT_BVH_SAH, non-parity fast mode, bvh_sah.h)
+    int bvh_mode = RT_BVH_REFERENCE;
+    int n_link_nodes = 0;
+    std::vector<uint8_t> sah_bvh;   // the SAH tree in the reference's node format (rt_debug_walk_bvh)
     FastTables fast;
     std::vector<float4> links;   // build_links(dnodes), empty when unavailable
     int fast_gen = 0;
@@ -927,6 +934,26 @@ float scene_extent(const rt_ctx* c) {
     return b < 1e30 ? (float)b : INFINITY;
 }
 
+// The fast mode's tree (bvh_sah.h) over the uploaded BVH's prims; child order: the one nearer the
+// camera first.
+int build_sah(rt_ctx* c, std::vector<rt_bvh_node>& out) {
+    rt_sah::Input in;
+    in.sph = (const rt_sphere*)c->host_buf[RT_BIND_SPHERES].data();
+    in.n_sph = c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere);
+    in.quad = (const rt_quad*)c->host_buf[RT_BIND_QUADS].data();
+    in.n_quad = c->host_buf[RT_BIND_QUADS].size() / sizeof(rt_quad);
+    in.med = (const rt_medium*)c->host_buf[RT_BIND_MEDIA].data();
+    in.n_med = c->host_buf[RT_BIND_MEDIA].size() / sizeof(rt_medium);
+    in.box = (const rt_box*)c->host_buf[RT_BIND_BOXES].data();
+    in.n_box = c->host_buf[RT_BIND_BOXES].size() / sizeof(rt_box);
+    in.ref = (const rt_bvh_node*)c->host_buf[RT_BIND_BVH].data();
+    in.n_ref = c->host_buf[RT_BIND_BVH].size() / sizeof(rt_bvh_node);
+    rt_sah::Builder b(in, 2, c->cam.camera_pos);
+    if (!b.build(out)) return set_err(c, RT_ERR_INVALID_ARG, "SAH BVH: the uploaded BVH's prims cannot be rebuilt");
+    if (out.size() > RT_MAX_RECORDS) return set_err(c, RT_ERR_LIMIT, "SAH BVH exceeds 65535 nodes");
+    return RT_OK;
+}
+
 int validate(rt_ctx* c) {
     if (c->validated) return RT_OK;
     size_t ns = c->host_buf[RT_BIND_SPHERES].size() / sizeof(rt_sphere);
@@ -977,7 +1004,21 @@ int validate(rt_ctx* c) {
     const std::vector<uint8_t>& BB = c->host_buf[RT_BIND_BOXES];
     c->fast = build_fast(c->dnodes, ns, (const rt_quad*)QB.data(), nq, (const rt_box*)BB.data(), nb);
     c->fast.ok = c->fast.ok && c->spec_ok && !c->uv_always;
-    c->links = build_links(c->dnodes);
+    if (c->bvh_mode == RT_BVH_SAH) {
+        std::vector<rt_bvh_node> sah;
+        int r = build_sah(c, sah);
+        if (r) return r;
+        std::vector<rt_dnode> dn;
+        r = thread_bvh(c, sah.data(), (int)sah.size(), dn);
+        if (r) return r;
+        c->links = build_links(dn);
+        c->n_link_nodes = (int)dn.size();
+        c->sah_bvh.assign((const uint8_t*)sah.data(), (const uint8_t*)(sah.data() + sah.size()));
+    } else {
+        c->links = build_links(c->dnodes);
+        c->n_link_nodes = c->n_dnodes;
+        c->sah_bvh.clear();
+    }
     c->pair_leaves = -1;
     c->fast_gen++;
     c->validated = true;
@@ -1020,14 +1061,30 @@ int ensure(rt_ctx* c, Device& d, DevBuf& b, size_t n) {
 
 // Runs the calls between ncclGroupStart and ncclGroupEnd and closes the group whatever they
 // return, so a failed Send / Recv / copy does not leave a group open on this thread (later
-// RCCL calls would be queued into it).  The body's error wins over GroupEnd's.
+// RCCL calls would be queued into it).  The body's error wins over GroupEnd's.  On an error the
+// context's communicators are then aborted (ncclCommAbort): the group may have
+// submitted a Send whose Recv was never queued (or the reverse), and a later stream
+// synchronisation would wait on that unmatched peer forever; aborting frees the queued work and
+// the next gather needs rt_comm_init (one process per GPU) or a fresh ncclCommInitAll.
+void abort_comms(rt_ctx* c);
 template <class F>
 int group_body(rt_ctx* c, F&& body) {
     const int r = body();
     const ncclResult_t e = rccl().GroupEnd();
+    if (r || e != ncclSuccess) abort_comms(c);
     if (r) return r;
     if (e != ncclSuccess) return set_err(c, RT_ERR_DEVICE, std::string("ncclGroupEnd: ") + rccl().GetErrorString(e));
     return RT_OK;
+}
+
+void abort_comms(rt_ctx* c) {
+    for (Device& d : c->devs) {
+        if (!d.comm) continue;
+        if (rccl().CommAbort) (void)rccl().CommAbort(d.comm);
+        d.comm = nullptr;
+    }
+    c->proc_comm = false;
+    c->comm_tried = false;   // a multi-device context makes its communicators again on the next gather
 }
 
 // Multi-device context: device k's stripe block (local_rows x W, in its padded slot) into
@@ -1489,6 +1546,7 @@ int rt_set_camera(rt_ctx* c, const float ubo[28]) {
     c->scene_extent = -1.0f;
     c->fd_cam = true;   // the camera's points and vectors within the fast-division regime's 2^20
     for (int i = 0; i < 28; i++) c->fd_cam = c->fd_cam && fd_coord(ubo[i]);
+    if (c->bvh_mode == RT_BVH_SAH) c->validated = false;   // the SAH tree orders children by the camera
     return RT_OK;
 }
 
@@ -1589,7 +1647,9 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     if (r) return r;
     rt_kernel_args a;
     std::memset(&a, 0, sizeof(a));
-    a.n_nodes = c->n_dnodes;
+    if (c->bvh_mode == RT_BVH_SAH && c->variant != 0 && c->variant != 39)
+        return set_err(c, RT_ERR_STATE, "the SAH BVH runs on the default kernel structure only");
+    a.n_nodes = c->n_link_nodes;
     a.watchdog_ticks = c->watchdog_ticks;
     a.chunk_wait_ticks = c->chunk_wait_ticks;
     int32_t lc = 0;
@@ -1612,7 +1672,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                     : 0;
     a.variant = c->variant;
     a.sm_batch = c->sm_batch;
-    a.walk_frac = c->walk_frac ? c->walk_frac : walk_frac_for(c->n_dnodes);
+    a.walk_frac = c->walk_frac ? c->walk_frac : walk_frac_for(c->n_link_nodes);
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);
@@ -1629,7 +1689,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
     a.debug_flags = c->debug_flags;
     a.n_lnode_f4 = (int)c->links.size();
-    plan_spine(c->links, c->n_dnodes, c->cam, c->spine, a);
+    plan_spine(c->links, c->n_link_nodes, c->cam, c->spine, a);
     // LDS plan of the link-format shapes (rt_kernel.hip rt_launch_render): from address 0 the
     // nodes, then the leaf records, the Perlin table (6 x 256 R32F), the media records with
     // their sphere boundaries, the spheres' intersection halves (A, B) and the canonical
@@ -1651,13 +1711,13 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.sm_frac = c->sm_frac ? c->sm_frac : (a.box_all_cmp ? 50 : 56);
     // the sphere-pair kernels (rt_kernel.hip leaf_prims_t SPAIR) for a BVH whose leaves are mostly
     // two spheres (scene 0: 485 spheres); measured slower where they are not
-    if (c->pair_leaves < 0) c->pair_leaves = pair_leaves_permille(c->links, c->n_dnodes);
+    if (c->pair_leaves < 0) c->pair_leaves = pair_leaves_permille(c->links, c->n_link_nodes);
     a.sph_pairs = (c->sphere_pairs && c->pair_leaves >= 500) ? 1 : 0;
     a.perlin_slot = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
     {
-        const size_t node_f4 = 2 * (size_t)c->n_dnodes;
+        const size_t node_f4 = 2 * (size_t)c->n_link_nodes;
         const size_t leaf_f4 = (size_t)a.n_lnode_f4 > node_f4 ? (size_t)a.n_lnode_f4 - node_f4 : 0;
         a.perlin_packed = (a.perlin_slot >= 0 && a.perlin_slot == c->perlin_pk_slot && c->perlin_pk) ? 1 : 0;
         // the Perlin table is staged in its packed form only (else its noise reads the texture)
@@ -1705,9 +1765,11 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         } else if (!fast_walk && a.n_lnode_f4 > 0) {
             if (tl) {
                 // the top levels, then the leaf records (8 B per leaf, read on every leaf visit) when
-                // they take at most half of the room, then the small tables the shading reads, and
-                // the sphere / compact box records when either takes at most 1/16 of the room (a
-                // few nodes' worth; option tl_small_lds)
+                // they take at most half of the room, then the small tables the shading reads; room
+                // is reserved for the sphere / compact box records that take at most 1/16 of it (a
+                // few nodes' worth), and each table is staged below whenever it still fits (option
+                // tl_small_lds; a larger table can fit after a node cap -- tests/test_gpu_adversarial.py
+                // forces both layouts)
                 const size_t room0 = cap - perlin_f4 - media_f4;
                 const size_t rsv = (c->tl_small_lds && sph_f4 && 16 * sph_f4 <= room0 ? sph_f4 : 0) +
                                    (c->tl_small_lds && box_f4 && 16 * box_f4 <= room0 ? box_f4 : 0);
@@ -1917,6 +1979,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                 return set_err(c, RT_ERR_DEVICE, std::string("kernel launch failed: ") +
                                                      hipGetErrorString(hipGetLastError()));
             HIPCHK(c, hipEventRecord(d.ring_ev[slot], d.stream));
+            if (&d == &c->devs[0]) c->last_launch[RT_LI_BVH_MODE] = c->bvh_mode;
         }
         HIPCHK(c, hipEventRecord(d.ev_stop, d.stream));
         d.timed = true;
@@ -2311,6 +2374,55 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
 #endif
         default: return set_err(c, RT_ERR_INVALID_ARG, "unknown option (A/B options need librtamd_ab.so)");
     }
+    return RT_OK;
+}
+
+int rt_set_bvh_mode(rt_ctx* c, int mode) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (mode != RT_BVH_REFERENCE && mode != RT_BVH_SAH) return set_err(c, RT_ERR_INVALID_ARG, "bad BVH mode");
+    if (mode != c->bvh_mode) {
+        c->bvh_mode = mode;
+        c->validated = false;   // validate() rebuilds the links (and a new fast_gen re-uploads them)
+    }
+    return RT_OK;
+}
+
+int rt_debug_walk_bvh(rt_ctx* c, void* out, size_t out_cap, size_t* nbytes) {
+    if (!c || !nbytes) return RT_ERR_INVALID_ARG;
+    if (!c->uploaded[RT_BIND_BVH]) return set_err(c, RT_ERR_STATE, "no BVH uploaded");
+    int r = validate(c);
+    if (r) return r;
+    const std::vector<uint8_t>& B = c->bvh_mode == RT_BVH_SAH ? c->sah_bvh : c->host_buf[RT_BIND_BVH];
+    *nbytes = B.size();
+    if (!out) return RT_OK;
+    if (out_cap < B.size()) return set_err(c, RT_ERR_LIMIT, "buffer too small");
+    std::memcpy(out, B.data(), B.size());
+    return RT_OK;
+}
+
+int rt_debug_build_sah_bvh(const void* spheres, size_t sph_bytes, const void* quads, size_t quad_bytes,
+                           const void* media, size_t med_bytes, const void* boxes, size_t box_bytes,
+                           const void* bvh, size_t bvh_bytes, int order, const float eye[3],
+                           float prim_cost, void* out, size_t out_cap, size_t* nbytes) {
+    if (!nbytes || (bvh_bytes && !bvh) || order < 0 || order > 2 || !(prim_cost > 0.0f)) return RT_ERR_INVALID_ARG;
+    rt_sah::Input in;
+    in.sph = (const rt_sphere*)spheres;
+    in.n_sph = spheres ? sph_bytes / sizeof(rt_sphere) : 0;
+    in.quad = (const rt_quad*)quads;
+    in.n_quad = quads ? quad_bytes / sizeof(rt_quad) : 0;
+    in.med = (const rt_medium*)media;
+    in.n_med = media ? med_bytes / sizeof(rt_medium) : 0;
+    in.box = (const rt_box*)boxes;
+    in.n_box = boxes ? box_bytes / sizeof(rt_box) : 0;
+    in.ref = (const rt_bvh_node*)bvh;
+    in.n_ref = bvh_bytes / sizeof(rt_bvh_node);
+    std::vector<rt_bvh_node> t;
+    rt_sah::Builder b(in, order, eye, prim_cost);
+    if (!b.build(t)) return RT_ERR_INVALID_ARG;
+    *nbytes = t.size() * sizeof(rt_bvh_node);
+    if (!out) return RT_OK;
+    if (out_cap < *nbytes) return RT_ERR_LIMIT;
+    std::memcpy(out, t.data(), *nbytes);
     return RT_OK;
 }
 

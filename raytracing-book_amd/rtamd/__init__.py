@@ -9,5 +9,5 @@ The compute path is the HIP kernel in lib/librtamd.so; nothing here computes pix
 from ._lib import RTError, amd, amd_ab, scene_lib  # noqa: F401
 from .render import (OPTIONS, RaytraceExecutor, RenderContext, comm_unique_id, deinterleave,  # noqa: F401
                      frame_rand_factors,
-                     local_rows, padded_local_rows, stripe_rows_of)
+                     local_rows, padded_local_rows, sah_bvh, stripe_rows_of)
 from .scene import SCENE_NAMES, Scene, SceneBuilder, save_png, spp_uniforms, tonemap_rgb8  # noqa: F401

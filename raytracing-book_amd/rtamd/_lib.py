@@ -108,6 +108,10 @@ def _amd_protos(L):
     _proto(L, "rt_debug_set_option", i, vp, i, i)
     _proto(L, "rt_debug_get_option", i, vp, i, c_int_p)
     _proto(L, "rt_debug_last_launch", i, vp, c_int_p, i)
+    _proto(L, "rt_set_bvh_mode", i, vp, i)
+    _proto(L, "rt_debug_walk_bvh", i, vp, vp, sz, ctypes.POINTER(sz))
+    _proto(L, "rt_debug_build_sah_bvh", i, vp, sz, vp, sz, vp, sz, vp, sz, vp, sz, i, c_float_p, f, vp, sz,
+           ctypes.POINTER(sz))
     return L
 
 

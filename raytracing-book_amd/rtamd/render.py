@@ -44,6 +44,27 @@ def comm_unique_id(lib=None):
     return buf.raw
 
 
+def sah_bvh(scene, order=2, eye=None, prim_cost=1.0, lib=None):
+    """rt_debug_build_sah_bvh (no device needed): the RT_BVH_SAH tree of a Scene's prims, as the
+    reference's BVH bytes (binding 1).  order 2 with the camera position (the default) is
+    rt_set_bvh_mode's tree."""
+    L = lib or _lib.amd()
+    b = scene.buffers
+    keep = [ctypes.create_string_buffer(b[k], len(b[k])) if b[k] else None for k in range(6)]
+    e = (ctypes.c_float * 3)(*(eye if eye is not None else scene.camera[4:7]))
+    n = ctypes.c_size_t()
+    args = (keep[0], len(b[0]), keep[2], len(b[2]), keep[3], len(b[3]), keep[4], len(b[4]), keep[1], len(b[1]),
+            int(order), e, float(prim_cost))
+    rc = L.rt_debug_build_sah_bvh(*args, None, 0, ctypes.byref(n))
+    if rc != 0:
+        raise RTError(rc, "rt_debug_build_sah_bvh failed")
+    out = ctypes.create_string_buffer(max(1, n.value))
+    rc = L.rt_debug_build_sah_bvh(*args, out, n.value, ctypes.byref(n))
+    if rc != 0:
+        raise RTError(rc, "rt_debug_build_sah_bvh failed")
+    return out.raw[:n.value]
+
+
 def local_rows(height, rank, world, stripe_rows):
     n_stripes = (height + stripe_rows - 1) // stripe_rows
     return sum(min(stripe_rows, height - s * stripe_rows) for s in range(rank, n_stripes, world))
@@ -82,7 +103,8 @@ OPTIONS = {"box_pretest": 1, "fastdiv": 2, "sph_lds": 3, "big_wg": 4, "chunk_tar
            "tl_leaf_lds": 16, "perlin_packed": 17, "sparse_stage": 18, "sphere_pairs": 19, "leaf_prefetch": 20, "tl_small_lds": 21, "shade_lds": 22, "kernel_variant": 100, "debug_flags": 101}
 # rt_debug_last_launch fields
 LAUNCH_FIELDS = ("shape", "block", "fastdiv", "pretest", "lds_bytes", "lds_nodes", "box_records", "staged",
-                 "chunks", "spine", "sparse", "sphere_pairs", "leaf_prefetch", "shade_lds", "walk_frac")
+                 "chunks", "spine", "sparse", "sphere_pairs", "leaf_prefetch", "shade_lds", "walk_frac", "bvh_mode")
+BVH_MODES = {"reference": 0, "sah": 1}   # rt.h RT_BVH_*
 SHAPES = {0: "fast-lds", 1: "fast-global", 2: "link-lds", 3: "meta-lds", 4: "meta-global", 5: "link-two-level"}
 
 
@@ -112,6 +134,18 @@ class RenderContext:
         self.sqrt_spp, self.recip_sqrt_spp = 1.0, 1.0
         for k, v in (options or {}).items():
             self.set_option(k, v)
+
+    def set_bvh_mode(self, mode):
+        """rt_set_bvh_mode: "reference" (default, bit-exact) or "sah" (non-parity fast mode)."""
+        self._check(self._L.rt_set_bvh_mode(self._h, BVH_MODES[mode] if isinstance(mode, str) else int(mode)))
+
+    def walk_bvh(self):
+        """rt_debug_walk_bvh: the BVH bytes (reference node format) the link walk runs on."""
+        n = ctypes.c_size_t()
+        self._check(self._L.rt_debug_walk_bvh(self._h, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(1, n.value))
+        self._check(self._L.rt_debug_walk_bvh(self._h, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
 
     def set_option(self, name, value):
         """rt_debug_set_option (rt_debug.h RT_OPTION_*)."""

@@ -178,7 +178,8 @@ LIN_RAW_TOL = 0.08   # every region, raw floats in the linear domain (round 2's 
 
 
 @pytest.mark.gpu
-def test_scene8_regions_match_gallery_full_size_gpu(gpu):
+@pytest.mark.parametrize("bvh", ["reference", "sah"])
+def test_scene8_regions_match_gallery_full_size_gpu(gpu, bvh):
     """Scene 8 at the gallery's own size (800x600) and 4096 spp through the HIP kernel
     (bit-exact with the oracle by the rest of the -m gpu suite): the fixed-geometry regions'
     means of the linearised bytes against book2_final(scene8).png, our image taken through
@@ -187,9 +188,11 @@ def test_scene8_regions_match_gallery_full_size_gpu(gpu):
     nor its max_depth (GUI slider 1-50, CLI default 5).  The blue fog region's blue channel
     pins the depth: 0.881 of the gallery at depth 5, 1.003 at 6, 1.105 at 7
     (tools/gallery_depth_probe.py, profiles/r02_gallery_depth_probe.log).  Tolerances:
-    GPU_REGION_TOL."""
+    GPU_REGION_TOL.  Also in the non-parity fast mode (bvh "sah", rt_set_bvh_mode): the same
+    anchors hold for the SAH tree's image (row f3's statistical gate)."""
     sc = rtamd.Scene(8, 800, 600, seed=1)
     ctx = rtamd.RenderContext(devices=(0,))
+    ctx.set_bvh_mode(bvh)
     ctx.upload_scene(sc)
     ctx.set_params(max_depth=6, spp=4096)
     ctx.resize(800, 600)
@@ -197,6 +200,7 @@ def test_scene8_regions_match_gallery_full_size_gpu(gpu):
     for k in range(0, 4096, 512):
         ctx.render(k + 1, rf[k:k + 512])
     img = ctx.read_image()
+    assert ctx.last_launch()["bvh_mode"] == rtamd.render.BVH_MODES[bvh]
     ctx.close()
     fx = FIX["scene8_regions"]["regions"]
     regs = gr.scene8_regions(sc.camera, 800, 600)
@@ -207,7 +211,7 @@ def test_scene8_regions_match_gallery_full_size_gpu(gpu):
     for name in ("glass", "metal", "blue_fog", "earth", "perlin"):
         ratio = lin_png[regs[name]].mean(0) / np.array(fx[name]["lin_mean"])
         report[name] = np.round(ratio, 3).tolist()
-    print("scene 8, 800x600, 4096 spp, depth 6, region mean / gallery (PNG pipeline):", report)
+    print(f"scene 8 ({bvh} BVH), 800x600, 4096 spp, depth 6, region mean / gallery (PNG pipeline):", report)
     bad = {k: v for k, v in report.items() if max(abs(x - 1.0) for x in v) > GPU_REGION_TOL[k]}
     assert not bad, f"region mean ratio outside GPU_REGION_TOL: {bad} (all: {report})"
     # The linear-domain bound kept beside the per-region PNG tolerances: the raw
@@ -240,7 +244,8 @@ def test_scene8_regions_match_gallery_full_size_gpu(gpu):
 
 
 @pytest.mark.gpu
-def test_scene6_blocks_match_gallery_4096spp_gpu(gpu):
+@pytest.mark.parametrize("bvh", ["reference", "sah"])
+def test_scene6_blocks_match_gallery_4096spp_gpu(gpu, bvh):
     """The Cornell box (book3_final(scene6).png, 600x600, the CLI's depth 5) at 4096 spp
     through the HIP kernel: 60x60 block means of the PNG bytes against the gallery's, the
     per-channel statement of the CPU suite's 64 spp oracle check (tests/test_oracle.py::
@@ -249,6 +254,7 @@ def test_scene6_blocks_match_gallery_4096spp_gpu(gpu):
     gb = np.array(FIX["scene6_block_means"])
     sc = rtamd.Scene(6, FIX["width"], FIX["height"], seed=1)
     ctx = rtamd.RenderContext(devices=(0,))
+    ctx.set_bvh_mode(bvh)
     ctx.upload_scene(sc)
     ctx.set_params(max_depth=5, spp=4096)
     ctx.resize(FIX["width"], FIX["height"])
@@ -263,7 +269,7 @@ def test_scene6_blocks_match_gallery_4096spp_gpu(gpu):
     d = ob - gb
     corr = float(np.corrcoef(gb.ravel(), ob.ravel())[0, 1])
     per_ch = [float(np.abs(d[..., c]).mean()) for c in range(3)]
-    print("scene 6, 600x600, 4096 spp: corr", round(corr, 5), "mean |block diff| per channel (of 255)",
+    print(f"scene 6 ({bvh} BVH), 600x600, 4096 spp: corr", round(corr, 5), "mean |block diff| per channel (of 255)",
           np.round(per_ch, 3).tolist(), "max", round(float(np.abs(d).max()), 3))
     # measured: corr 0.99998, mean |diff| 0.133 / 0.139 / 0.136 of 255, max 0.79
     assert corr > 0.9999, corr
@@ -271,9 +277,10 @@ def test_scene6_blocks_match_gallery_4096spp_gpu(gpu):
     assert np.abs(d).max() < 2.0, np.abs(d).max()
 
 
-def _render_gpu(sid, w, h, spp, depth):
+def _render_gpu(sid, w, h, spp, depth, bvh="reference"):
     sc = rtamd.Scene(sid, w, h, seed=1)
     ctx = rtamd.RenderContext(devices=(0,))
+    ctx.set_bvh_mode(bvh)
     ctx.upload_scene(sc)
     ctx.set_params(max_depth=depth, spp=spp)
     ctx.resize(w, h)
@@ -286,7 +293,8 @@ def _render_gpu(sid, w, h, spp, depth):
 
 
 @pytest.mark.gpu
-def test_scene0_fixed_spheres_match_gallery_gpu(gpu):
+@pytest.mark.parametrize("bvh", ["reference", "sah"])
+def test_scene0_fixed_spheres_match_gallery_gpu(gpu, bvh):
     """Scene 0's three fixed spheres (book1_final(scene0).png, 800x600) at 4096 spp through
     the HIP kernel: means of the linearised bytes over the pixels whose ray meets them above
     the random small spheres' layer, at the CLI's depth 5 (depth 6 moves glass from 1.09-1.12
@@ -296,7 +304,7 @@ def test_scene0_fixed_spheres_match_gallery_gpu(gpu):
     sphere refracts the unseeded small spheres (not the gallery's): 1.09-1.12."""
     depth = 5
     fx = FIX["scene0_regions"]
-    sc, img = _render_gpu(0, fx["width"], fx["height"], 4096, depth)
+    sc, img = _render_gpu(0, fx["width"], fx["height"], 4096, depth, bvh)
     regs = gr.scene0_regions(sc.camera, fx["width"], fx["height"])
     lin = np.clip(np.nan_to_num(img[..., :3], nan=0.0), 0.0, 1.0)
     report = {}
@@ -304,6 +312,6 @@ def test_scene0_fixed_spheres_match_gallery_gpu(gpu):
         m = regs[name]
         assert abs(int(m.sum()) - r["n_pixels"]) == 0, name   # the fixture's masks
         report[name] = np.round(lin[m].mean(0) / np.array(r["lin_mean"]), 3).tolist()
-    print(f"scene 0, 800x600, 4096 spp, depth {depth}, region mean / gallery:", report)
+    print(f"scene 0 ({bvh} BVH), 800x600, 4096 spp, depth {depth}, region mean / gallery:", report)
     assert max(abs(x - 1.0) for n in ("diffuse", "metal") for x in report[n]) <= 0.03, report
     assert max(abs(x - 1.0) for x in report["glass"]) <= LIN_TOL, report

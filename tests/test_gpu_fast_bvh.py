@@ -1,0 +1,99 @@
+"""The non-parity fast mode on the GPU (row f3; rt.h rt_set_bvh_mode(RT_BVH_SAH)).
+
+* Bit for bit against the oracle walking the same SAH tree: the kernel does not care which
+  BVH it walks, so in the fast mode it is still exact -- against the reference semantics
+  applied to the SAH tree (rt_debug_walk_bvh hands the tree to the oracle).
+* Statistically against the reference BVH at equal samples (scenes 0, 6, 8): the fast mode
+  changes where a medium's rand() draws fall in the visit sequence (and how exact ties
+  resolve), not the estimator.  Block means of the two images agree within the tolerance
+  below; the gallery anchors run in both modes (tests/test_gallery_anchor.py, bvh=sah).
+* The release default stays the parity path: a context that never calls rt_set_bvh_mode
+  walks the uploaded BVH (rt_debug_last_launch bvh_mode 0).
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+import rtamd
+from helpers import bit_equal
+from test_fast_bvh import with_bvh
+
+pytestmark = pytest.mark.gpu
+
+
+def render(scene, frames, bvh="reference", depth=5, spp=None, chunk=512):
+    ctx = rtamd.RenderContext(devices=(0,))
+    if bvh != "reference":
+        ctx.set_bvh_mode(bvh)
+    ctx.upload_scene(scene)
+    ctx.set_params(max_depth=depth, spp=spp or frames)
+    ctx.resize(scene.width, scene.height)
+    rf = rtamd.frame_rand_factors(1, 0, frames)
+    for k in range(0, frames, chunk):
+        ctx.render(k + 1, rf[k:k + chunk])
+    img = ctx.read_image()
+    info = ctx.last_launch()
+    walked = ctx.walk_bvh()
+    ctx.close()
+    return img, info, walked
+
+
+@pytest.mark.parametrize("sid,w,h,frames", [(8, 64, 36, 4), (0, 64, 36, 4), (6, 48, 48, 4), (7, 48, 48, 4),
+                                            (3, 48, 27, 4), (2, 48, 27, 2), (9, 48, 27, 4)])
+def test_sah_mode_bit_exact_against_oracle_on_the_sah_tree(gpu, sid, w, h, frames):
+    sc = rtamd.Scene(sid, w, h, seed=1)
+    img, info, walked = render(sc, frames, "sah")
+    assert info["bvh_mode"] == 1
+    assert walked == rtamd.sah_bvh(sc)   # the context's tree is the context-free builder's
+    ref = pyoracle.render(pyoracle.OracleScene(with_bvh(sc, walked), max_depth=5, spp=frames),
+                          rtamd.frame_rand_factors(1, 0, frames), nthreads=4)
+    assert bit_equal(img, ref)
+
+
+def test_default_is_the_reference_bvh(gpu):
+    sc = rtamd.Scene(8, 32, 18, seed=1)
+    img, info, walked = render(sc, 2)
+    assert info["bvh_mode"] == 0 and walked == sc.buffers[1]
+    ref = pyoracle.render(pyoracle.OracleScene(sc, max_depth=5, spp=2), rtamd.frame_rand_factors(1, 0, 2), nthreads=4)
+    assert bit_equal(img, ref)
+    # switching back to the reference BVH on a context restores the exact path
+    ctx = rtamd.RenderContext(devices=(0,))
+    ctx.set_bvh_mode("sah")
+    ctx.upload_scene(sc)
+    ctx.set_params(max_depth=5, spp=2)
+    ctx.resize(32, 18)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 2))
+    ctx.set_bvh_mode("reference")
+    ctx.resize(32, 18)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 2))
+    again = ctx.read_image()
+    assert ctx.last_launch()["bvh_mode"] == 0
+    ctx.close()
+    assert bit_equal(again, ref)
+
+
+# Block means (16x16 px blocks) of the two modes' images at 320x180, 1024 spp, depth 5: the
+# relative difference per block and channel, over blocks whose reference mean is at least 0.02
+# (dark blocks are all relative noise).  Tolerances: the measured worst + margin (profiles/
+# r05_fast_bvh_stats.log, printed below); the global means within 0.5%.
+BLOCK_TOL = {0: 0.03, 6: 0.05, 8: 0.05}
+
+
+@pytest.mark.parametrize("sid", [0, 6, 8])
+def test_sah_mode_statistics_match_the_reference_bvh(gpu, sid):
+    sc = rtamd.Scene(sid, 320, 180, seed=1)
+    a, ia, _ = render(sc, 1024, "reference", spp=1024)
+    b, ib, _ = render(sc, 1024, "sah", spp=1024)
+    assert ia["bvh_mode"] == 0 and ib["bvh_mode"] == 1
+    A = np.nan_to_num(a[..., :3].astype(np.float64))
+    B = np.nan_to_num(b[..., :3].astype(np.float64))
+    g = np.abs(B.mean((0, 1)) / A.mean((0, 1)) - 1.0)
+    S = 16
+    ba = A[:180 // S * S].reshape(180 // S, S, 320 // S, S, 3).mean((1, 3))
+    bb = B[:180 // S * S].reshape(180 // S, S, 320 // S, S, 3).mean((1, 3))
+    ok = ba > 0.02
+    rel = np.abs(bb[ok] / ba[ok] - 1.0)
+    print(f"scene {sid}: global mean ratio - 1 {np.round(g, 4).tolist()}, block rel diff max {rel.max():.4f} "
+          f"p99 {np.quantile(rel, 0.99):.4f} mean {rel.mean():.4f} over {ok.sum()} block-channels")
+    assert np.all(g < 0.005), g
+    assert rel.max() < BLOCK_TOL[sid], rel.max()

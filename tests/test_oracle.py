@@ -100,6 +100,11 @@ def test_builtin_special_cases():
     assert r[0] == np.inf and r[1] == -np.inf and r[2] == 0.0 and np.isnan(r[3:]).all()
     wide = np.exp2(np.random.default_rng(3).uniform(-126, 127, 100000)).astype(np.float32)
     assert (_ulp_err(pyoracle.eval_builtin("inversesqrt", wide), 1.0 / np.sqrt(wide.astype(np.float64))) <= 2.0).all()
+    # subnormals (the bit-level guess alone was ~2x off there): scaled into range first
+    subn = np.concatenate([np.exp2(np.random.default_rng(4).uniform(-149, -126, 20000)).astype(np.float32),
+                           np.array([1e-45, 1.1754942e-38, 5e-39], np.float32)])
+    assert (subn > 0).all() and (subn < np.float32(1.17549435e-38)).all()
+    assert (_ulp_err(pyoracle.eval_builtin("inversesqrt", subn), 1.0 / np.sqrt(subn.astype(np.float64))) <= 2.0).all()
 
 
 def test_builtin_atan2_and_fract():
