@@ -35,6 +35,10 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
  * (types | next address << 8, prims) as uint2.  *n_f4 = its float4 count, 0 when
  * there is no BVH. */
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4);
+/* The same with the box pre-test nodes (option box_vnodes): vbox = 6 floats per box (its
+ * pre-test bounds: xmin, xmax, ymin, ymax, zmin, zmax); *n_nodes = tree + pre-test nodes. */
+int rt_debug_link_nodes_vbox(const void* bvh, size_t nbytes, const float* vbox, int n_box, void* out,
+                             size_t out_cap, int* n_f4, int* n_nodes);
 
 /* Host-only: the packed Perlin table rt_upload_texture keeps beside an R32F 6 x 256 texture
  * whose perm columns (3..5) hold whole numbers 0..255: 256 float4 (ranvec x, y, z; the three
@@ -116,6 +120,9 @@ enum {
     RT_OPTION_SHADE_LDS = 22,           /* shading tables in LDS: sphere and compact box
                                            materials, texture descriptors, small texture
                                            slots (1)                                        */
+    RT_OPTION_BOX_VNODES = 23,          /* compact-box kernels: each all-box leaf's box bounds
+                                           pre-tests as nodes of the walk, the leaf stage
+                                           testing only the boxes they pass (1)            */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };
@@ -135,7 +142,8 @@ int rt_debug_get_option(struct rt_ctx* ctx, int option, int* value);
  *   out[11] sphere-pair kernel (1 = a two-sphere leaf's spheres tested at once)
  *   out[12] leaf record prefetch  out[13] shading tables in LDS (bits)  out[14] walk threshold
  *   out[15] the BVH the walk ran on: RT_BVH_REFERENCE (0) or RT_BVH_SAH (1, rt_set_bvh_mode)
- * n <= 16 ints are written; returns RT_ERR_STATE before the first render. */
+ *   out[16] box pre-test nodes in the walk (option box_vnodes; 0 = none)
+ * n <= 20 ints are written; returns RT_ERR_STATE before the first render. */
 int rt_debug_last_launch(struct rt_ctx* ctx, int* out, int n);
 
 /* The BVH the link walk of ctx uses, in the reference's node format (rt_bvh_node): the

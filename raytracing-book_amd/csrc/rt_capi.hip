@@ -141,6 +141,16 @@ struct rt_ctx {
     int bvh_mode = RT_BVH_REFERENCE;
     int n_link_nodes = 0;
     std::vector<uint8_t> sah_bvh;   // the SAH tree in the reference's node format (rt_debug_walk_bvh)
+    std::vector<rt_dnode> walk_dn;  // threaded nodes of the BVH the link walk uses (reference or SAH)
+    // the links the launch walks: c->links, or (option box_vnodes) the same with every all-box leaf's
+    // box pre-tests as nodes of the walk (build_links with vbox); rebuilt when the margin changes
+    std::vector<float4> walk_links;
+    int n_walk_nodes = 0;
+    bool walk_v = false;
+    float walk_v_margin = -1.0f;
+    bool walk_stale = true;
+    std::vector<float4> boxc_host;  // the compact box records (host copy of Device::dboxc)
+    bool box_vnodes = true;         // option box_vnodes
     FastTables fast;
     std::vector<float4> links;   // build_links(dnodes), empty when unavailable
     int fast_gen = 0;
@@ -377,9 +387,11 @@ bool boxes_nest(const std::vector<rt_dnode>& dn) {
 // sequence (tests/test_link_nodes.py), and the top levels every ray walks sit at the
 // lowest addresses, the part a two-level launch stages in LDS.  Empty when there is
 // no BVH or it has more nodes than 16-bit indices address.
-std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
+std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vector<float>* vbox = nullptr,
+                                int* n_nodes_out = nullptr) {
     std::vector<float4> out;
     const size_t n = dn.size();
+    if (n_nodes_out) *n_nodes_out = 0;
     if (n == 0 || n > RT_LINK_MAX_NODES) return out;
     auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
     std::vector<uint32_t> pos(n, 0xFFFFFFFFu), order;
@@ -396,32 +408,70 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn) {
         order.push_back(l);
     }
     if (order.size() != n) return out;
+    // Box pre-tests as nodes (vbox: 6 floats per box, its bounds grown by the pre-test's margin,
+    // rt_kernel.hip leaf_prims_t): a leaf of one or two boxes becomes a chain of one node per box
+    // whose hit leads to that box's own leaf record -- the box tested alone, marked pre-tested
+    // (RT_LINK_PRETESTED) -- and whose miss (or the record's continuation) leads to the next box's
+    // node, after the last one to the leaf's skip node.  The walk meets the boxes in the same
+    // order, each node test is the pre-test itself (the same slab function on the same floats
+    // under the same ray_t), and a box whose pre-test misses is one the exact test rejects, so
+    // every lane tests the same boxes with the same results -- only the pre-test moves from the
+    // leaf stage into the walk.  The chain nodes follow the tree's nodes.
+    const size_t nbox = vbox ? vbox->size() / 6 : 0;
+    std::vector<uint32_t> vfirst(n, 0xFFFFFFFFu);   // leaf k's first chain node (0xFFFFFFFF: not expanded)
+    size_t nv = 0;
+    for (size_t k = 0; k < n && vbox; k++) {
+        if (!is_leaf(k)) continue;
+        const uint32_t t0 = (dn[k].meta >> 16) & 0xFu, t1 = (dn[k].meta >> 20) & 0xFu;
+        const uint32_t p0 = dn[k].prims & 0xFFFFu, p1 = dn[k].prims >> 16;
+        if (t0 != RT_MODEL_BOX || (t1 != RT_MODEL_BOX && t1 != 0) || p0 >= nbox || (t1 && p1 >= nbox)) continue;
+        vfirst[k] = (uint32_t)(n + nv);
+        nv += t1 ? 2 : 1;
+    }
+    const size_t N = n + nv;
+    if (N > RT_LINK_MAX_NODES) return build_links(dn, nullptr, n_nodes_out);
     size_t nl = 0;
-    for (size_t k = 0; k < n; k++) nl += is_leaf(k);
-    out.assign(2 * n + (nl + 1) / 2, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    uint2* leaves = reinterpret_cast<uint2*>(out.data() + 2 * n);
+    for (size_t k = 0; k < n; k++)
+        if (is_leaf(k)) nl += vfirst[k] == 0xFFFFFFFFu ? 1 : (((dn[k].meta >> 20) & 0xFu) ? 2 : 1);
+    out.assign(2 * N + (nl + 1) / 2, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    uint2* leaves = reinterpret_cast<uint2*>(out.data() + 2 * N);
     auto f = [](uint32_t u) {
         float x;
         std::memcpy(&x, &u, 4);
         return x;
+    };
+    auto put = [&](size_t at, float x0, float x1, float y0, float y1, float z0, float z1, uint32_t hit, uint32_t miss) {
+        out[2 * at] = make_float4(x0, x1, y0, y1);
+        out[2 * at + 1] = make_float4(z0, z1, f(hit), f(miss));
     };
     uint32_t li = 0;
     for (size_t k = 0; k < n; k++) {
         const rt_dnode& d = dn[k];
         const uint32_t skip = d.meta & 0xFFFFu;
         const uint32_t skip_at = skip == RT_NODE_END ? RT_LINK_END : 32u * pos[skip];
+        const uint32_t next_end = skip == RT_NODE_END ? RT_LINK_NEXT_END : skip_at;
         uint32_t hit;
-        if (is_leaf(k)) {
+        if (is_leaf(k) && vfirst[k] != 0xFFFFFFFFu) {
+            const uint32_t v0 = vfirst[k];
+            const bool two = ((d.meta >> 20) & 0xFu) != 0;
+            hit = 32u * v0;
+            for (int j = 0; j < (two ? 2 : 1); j++) {
+                const uint32_t b = j ? d.prims >> 16 : d.prims & 0xFFFFu;
+                const float* g = vbox->data() + 6 * (size_t)b;
+                const bool last = !two || j == 1;
+                const uint32_t cont = last ? skip_at : 32u * (v0 + 1);
+                put(v0 + j, g[0], g[1], g[2], g[3], g[4], g[5], RT_LINK_LEAF | li, cont);
+                leaves[li++] = make_uint2((RT_MODEL_BOX | RT_LINK_PRETESTED) | (last ? next_end : cont) << 8, b);
+            }
+        } else if (is_leaf(k)) {
             hit = RT_LINK_LEAF | li;
-            const uint32_t next = skip == RT_NODE_END ? RT_LINK_NEXT_END : skip_at;
-            leaves[li++] = make_uint2(((d.meta >> 16) & 0xFFu) | next << 8, d.prims);
+            leaves[li++] = make_uint2(((d.meta >> 16) & 0xFFu) | next_end << 8, d.prims);
         } else {
             hit = 32u * pos[k + 1];
         }
-        const uint32_t at = pos[k];
-        out[2 * at] = make_float4(d.xmin, d.xmax, d.ymin, d.ymax);
-        out[2 * at + 1] = make_float4(d.zmin, d.zmax, f(hit), f(skip_at));
+        put(pos[k], d.xmin, d.xmax, d.ymin, d.ymax, d.zmin, d.zmax, hit, skip_at);
     }
+    if (n_nodes_out) *n_nodes_out = (int)N;
     return out;
 }
 
@@ -1014,11 +1064,14 @@ int validate(rt_ctx* c) {
         c->links = build_links(dn);
         c->n_link_nodes = (int)dn.size();
         c->sah_bvh.assign((const uint8_t*)sah.data(), (const uint8_t*)(sah.data() + sah.size()));
+        c->walk_dn.swap(dn);
     } else {
         c->links = build_links(c->dnodes);
         c->n_link_nodes = c->n_dnodes;
         c->sah_bvh.clear();
+        c->walk_dn = c->dnodes;
     }
+    c->walk_stale = true;
     c->pair_leaves = -1;
     c->fast_gen++;
     c->validated = true;
@@ -1413,7 +1466,10 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
             }
         }
         c->fd_ok[binding] = fd;
-        if (binding == RT_BIND_BOXES) c->n_boxc_ok = n_cmp;
+        if (binding == RT_BIND_BOXES) {
+            c->n_boxc_ok = n_cmp;
+            c->boxc_host = boxc;
+        }
     }
     if (binding == RT_BIND_SPHERES) {
         const rt_sphere* sp = (const rt_sphere*)bytes;
@@ -1649,7 +1705,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     std::memset(&a, 0, sizeof(a));
     if (c->bvh_mode == RT_BVH_SAH && c->variant != 0 && c->variant != 39)
         return set_err(c, RT_ERR_STATE, "the SAH BVH runs on the default kernel structure only");
-    a.n_nodes = c->n_link_nodes;
     a.watchdog_ticks = c->watchdog_ticks;
     a.chunk_wait_ticks = c->chunk_wait_ticks;
     int32_t lc = 0;
@@ -1672,7 +1727,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                     : 0;
     a.variant = c->variant;
     a.sm_batch = c->sm_batch;
-    a.walk_frac = c->walk_frac ? c->walk_frac : walk_frac_for(c->n_link_nodes);
+    a.walk_frac = c->walk_frac ? c->walk_frac : walk_frac_for(c->n_link_nodes);   // by the tree, not the pre-test nodes
     const FastTables& F = c->fast;
     a.fast_ok = F.ok ? 1 : 0;
     a.n_f2inner = (int)(F.inner2.size() / 4);
@@ -1688,8 +1743,42 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     std::memcpy(a.fl_medium, F.fl_medium, sizeof(a.fl_medium));
     std::memcpy(a.fl_rank, F.fl_rank, sizeof(a.fl_rank));
     a.debug_flags = c->debug_flags;
-    a.n_lnode_f4 = (int)c->links.size();
-    plan_spine(c->links, c->n_link_nodes, c->cam, c->spine, a);
+    // the links the launch walks: with the box pre-test nodes (option box_vnodes) when every box has a
+    // compact record and the pre-test is on (its margin is the nodes' growth: rebuilt when it changes)
+    {
+        const size_t nb = c->host_buf[RT_BIND_BOXES].size() / sizeof(rt_box);
+        const bool all_cmp = c->compact_boxes && nb > 0 && c->n_boxc_ok == (int)nb;
+        const bool use_v = c->box_vnodes && all_cmp && a.box_margin > 0.0f && (c->variant == 0 || c->variant == 39) &&
+                           c->boxc_host.size() == nb * RT_BOXC_F4;
+        if (c->walk_stale || use_v != c->walk_v || (use_v && a.box_margin != c->walk_v_margin)) {
+            if (use_v) {
+                // the kernel's pre-test bounds (leaf_prims_t): compact record c0 = (mn.x, mn.y, mn.z,
+                // mx.x), c1 = (mx.y, mx.z, ..), each grown by the margin with the same float operations
+                const float m = a.box_margin;
+                std::vector<float> vb(6 * nb);
+                for (size_t b = 0; b < nb; b++) {
+                    const float4 c0 = c->boxc_host[b * RT_BOXC_F4], c1 = c->boxc_host[b * RT_BOXC_F4 + 1];
+                    const float g[6] = {c0.x - m, c0.w + m, c0.y - m, c1.x + m, c0.z - m, c1.y + m};
+                    std::memcpy(&vb[6 * b], g, sizeof(g));
+                }
+                int nn = 0;
+                c->walk_links = build_links(c->walk_dn, &vb, &nn);
+                c->n_walk_nodes = nn;
+            } else {
+                c->walk_links = c->links;
+                c->n_walk_nodes = c->n_link_nodes;
+            }
+            c->walk_v = use_v;
+            c->walk_v_margin = use_v ? a.box_margin : -1.0f;
+            c->walk_stale = false;
+            c->pair_leaves = -1;
+            c->fast_gen++;   // re-upload the links (rt_render's device loop)
+        }
+        a.box_vnodes = c->walk_v && c->n_walk_nodes > c->n_link_nodes ? 1 : 0;
+    }
+    a.n_nodes = c->n_walk_nodes;
+    a.n_lnode_f4 = (int)c->walk_links.size();
+    plan_spine(c->walk_links, c->n_walk_nodes, c->cam, c->spine, a);
     // LDS plan of the link-format shapes (rt_kernel.hip rt_launch_render): from address 0 the
     // nodes, then the leaf records, the Perlin table (6 x 256 R32F), the media records with
     // their sphere boundaries, the spheres' intersection halves (A, B) and the canonical
@@ -1711,13 +1800,13 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.sm_frac = c->sm_frac ? c->sm_frac : (a.box_all_cmp ? 50 : 56);
     // the sphere-pair kernels (rt_kernel.hip leaf_prims_t SPAIR) for a BVH whose leaves are mostly
     // two spheres (scene 0: 485 spheres); measured slower where they are not
-    if (c->pair_leaves < 0) c->pair_leaves = pair_leaves_permille(c->links, c->n_link_nodes);
+    if (c->pair_leaves < 0) c->pair_leaves = pair_leaves_permille(c->walk_links, c->n_walk_nodes);
     a.sph_pairs = (c->sphere_pairs && c->pair_leaves >= 500) ? 1 : 0;
     a.perlin_slot = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
     {
-        const size_t node_f4 = 2 * (size_t)c->n_link_nodes;
+        const size_t node_f4 = 2 * (size_t)c->n_walk_nodes;
         const size_t leaf_f4 = (size_t)a.n_lnode_f4 > node_f4 ? (size_t)a.n_lnode_f4 - node_f4 : 0;
         a.perlin_packed = (a.perlin_slot >= 0 && a.perlin_slot == c->perlin_pk_slot && c->perlin_pk) ? 1 : 0;
         // the Perlin table is staged in its packed form only (else its noise reads the texture)
@@ -1876,7 +1965,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             int rf = dev_alloc_copy(c, d, d.finfo, F.info.data(), F.info.size() * sizeof(uint32_t));
             if (!rf) rf = dev_alloc_copy(c, d, d.f2inner, F.inner2.data(), F.inner2.size() * sizeof(float4));
             if (!rf) rf = dev_alloc_copy(c, d, d.f2leaves, F.leaves2.data(), F.leaves2.size() * sizeof(uint2));
-            if (!rf) rf = dev_alloc_copy(c, d, d.links, c->links.data(), c->links.size() * sizeof(float4));
+            if (!rf) rf = dev_alloc_copy(c, d, d.links, c->walk_links.data(), c->walk_links.size() * sizeof(float4));
             if (rf) return rf;
             d.fast_gen = c->fast_gen;
         }
@@ -1979,7 +2068,10 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                 return set_err(c, RT_ERR_DEVICE, std::string("kernel launch failed: ") +
                                                      hipGetErrorString(hipGetLastError()));
             HIPCHK(c, hipEventRecord(d.ring_ev[slot], d.stream));
-            if (&d == &c->devs[0]) c->last_launch[RT_LI_BVH_MODE] = c->bvh_mode;
+            if (&d == &c->devs[0]) {
+                c->last_launch[RT_LI_BVH_MODE] = c->bvh_mode;
+                c->last_launch[RT_LI_VNODES] = a.box_vnodes ? c->n_walk_nodes - c->n_link_nodes : 0;
+            }
         }
         HIPCHK(c, hipEventRecord(d.ev_stop, d.stream));
         d.timed = true;
@@ -2182,6 +2274,24 @@ int rt_debug_box_records(const void* boxes, size_t nbytes, void* out, size_t out
     return RT_OK;
 }
 
+int rt_debug_link_nodes_vbox(const void* bvh, size_t nbytes, const float* vbox, int n_box, void* out,
+                             size_t out_cap, int* n_f4, int* n_nodes) {
+    if (!bvh || !n_f4 || !n_nodes || nbytes % sizeof(rt_bvh_node) || n_box < 0 || (n_box && !vbox))
+        return RT_ERR_INVALID_ARG;
+    std::vector<rt_dnode> dn;
+    rt_ctx tmp;
+    int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
+    if (r) return r;
+    const std::vector<float> vb(vbox, vbox + 6 * (size_t)n_box);
+    const std::vector<float4> L = build_links(dn, &vb, n_nodes);
+    *n_f4 = (int)L.size();
+    if (out) {
+        if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
+        std::memcpy(out, L.data(), L.size() * sizeof(float4));
+    }
+    return RT_OK;
+}
+
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4) {
     if (!bvh || !n_f4 || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
     std::vector<rt_dnode> dn;
@@ -2322,6 +2432,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_LEAF_PREFETCH: c->leaf_prefetch = v != 0; break;
         case RT_OPTION_TL_SMALL_LDS: c->tl_small_lds = v != 0; break;
         case RT_OPTION_SHADE_LDS: c->shade_lds = v != 0; break;
+        case RT_OPTION_BOX_VNODES: c->box_vnodes = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2359,6 +2470,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_LEAF_PREFETCH: *v = c->leaf_prefetch; break;
         case RT_OPTION_TL_SMALL_LDS: *v = c->tl_small_lds; break;
         case RT_OPTION_SHADE_LDS: *v = c->shade_lds; break;
+        case RT_OPTION_BOX_VNODES: *v = c->box_vnodes; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

@@ -72,6 +72,9 @@ static_assert(sizeof(rt_dnode) == 32, "device node is 32 B");
 #define RT_LINK_END 0xFFFFFFFFu
 #define RT_LINK_NEXT_END 0xFFFFFFu
 #define RT_LINK_MAX_NODES 65535
+// In a leaf record's type byte: slot 0's box was pre-tested by a node of the walk (option box_vnodes,
+// rt_capi.hip build_links), so the leaf stage skips its bounds pre-test
+#define RT_LINK_PRETESTED 8u
 
 struct rt_dtex {
     const void* data;   // RGBA8 (uint32) or R32F
@@ -120,6 +123,7 @@ struct rt_kernel_args {
     int sm_frac;                 // or this many 64ths of the lanes with a walk (or none runs)
     int walk_frac;               // render_sm: a round's node walk stops once this many 64ths of its lanes
                                  // hold a leaf or ended (64: all of them)
+    int box_vnodes;              // the links carry box pre-test nodes (leaf records marked RT_LINK_PRETESTED)
     int leaf_pf;                 // BOXC kernels: the leaf stage prefetches each slot's record (spheres, boxes
                                  // and media all staged in LDS; rt_kernel.hip leaf_prims_t)
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)
@@ -188,7 +192,7 @@ struct rt_kernel_args {
 
 // What rt_launch_render launched (rt_debug_last_launch)
 enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
-       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_LEAF_PF, RT_LI_SHADE_LDS, RT_LI_WALK_FRAC, RT_LI_BVH_MODE, RT_LI_N = 16 };
+       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_LEAF_PF, RT_LI_SHADE_LDS, RT_LI_WALK_FRAC, RT_LI_BVH_MODE, RT_LI_VNODES, RT_LI_N = 20 };
 
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)

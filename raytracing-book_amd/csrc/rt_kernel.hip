@@ -609,6 +609,13 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
     for (int s = 0; s < 2; s++) {
         int ty = (int)((meta >> (16 + 4 * s)) & 0xFu);
         int ix = (int)((prims >> (16 * s)) & 0xFFFFu);
+        // a box whose bounds pre-test already ran as a node of the walk (P.box_vnodes, rt_capi.hip
+        // build_links; its leaf record's RT_LINK_PRETESTED bit): the same test, not repeated
+        bool pretested = false;
+        if (s == 0 && BOXC) {
+            pretested = (ty & RT_LINK_PRETESTED) != 0;
+            ty &= 7;
+        }
         if (STATS) {
             st_pred(st, ty == RT_MODEL_SPHERE, ST_SPH_IT, ST_SPH_LN);
             st_pred(st, ty == RT_MODEL_QUAD, ST_QUAD_IT, ST_QUAD_LN);
@@ -680,7 +687,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
                 r2 = ldg(cr + 2);
             }
             bool maybe = true;
-            if (P.box_margin > 0.0f && (BOXC || fin)) {
+            if (P.box_margin > 0.0f && (BOXC || fin) && !pretested) {
                 // the box's bounds grown by box_margin (rt_device.h): a ray that misses them
                 // misses every face the exact test below would accept
                 const float m = P.box_margin;

@@ -30,7 +30,8 @@ from helpers import bit_equal, mismatch_report
 pytestmark = pytest.mark.gpu
 
 CASES = adversarial.cases()
-OFF = [{}, {"box_pretest": 0}, {"fastdiv": 0}, {"compact_boxes": 0}, {"spine": 0}, {"shade_lds": 0}]
+OFF = [{}, {"box_pretest": 0}, {"fastdiv": 0}, {"compact_boxes": 0}, {"spine": 0}, {"shade_lds": 0},
+       {"box_vnodes": 0}]
 
 
 def oracle(case):

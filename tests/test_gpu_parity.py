@@ -184,3 +184,28 @@ def test_shared_reciprocal_division_bit_exact(gpu):
     for fn in (101, 102):
         bad = np.flatnonzero(outs[fn] != outs[100])
         assert bad.size == 0, (fn, bad.size, num[bad[:4]], den[bad[:4]])
+
+
+@pytest.mark.parametrize("opts,expect", [({}, True), ({"box_vnodes": 0}, False), ({"box_pretest": 0}, False)])
+def test_box_pretest_nodes_match_oracle(gpu, opts, expect):
+    """Round 5: scene 8's ground boxes' bounds pre-tests run as nodes of the
+    walk (option box_vnodes, on by default in the compact-box kernels when the pre-test is on);
+    the leaf stage tests only the boxes they pass.  Bit for bit against the oracle either way, and
+    the launch reports the chain nodes it walked."""
+    s = rtamd.Scene(8, 48, 27, seed=1)
+    ref = oracle_image(s, 6, max_depth=5)
+    ctx = rtamd.RenderContext(devices=(0,), options=opts)
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=6)
+    ctx.resize(48, 27)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 6))
+    out = ctx.read_image()
+    info = ctx.last_launch()
+    ctx.close()
+    assert (info["box_vnodes"] > 0) == expect, info
+    if expect:   # one node per box of the all-box leaves (390 of scene 8's 400 boxes)
+        from test_fast_tables import is_leaf, threaded
+        n = sum((2 if (int(nd["meta"]) >> 20) & 0xF else 1) for nd in threaded(s)
+                if is_leaf(nd) and (int(nd["meta"]) >> 16) & 0xF == 4 and (int(nd["meta"]) >> 20) & 0xF in (0, 4))
+        assert info["box_vnodes"] == n == 390, (info, n)
+    assert bit_equal(out, ref), mismatch_report(out, ref)

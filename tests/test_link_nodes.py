@@ -162,3 +162,93 @@ def test_link_format_reaches_the_16_bit_node_limit(n_leaves):
         for p in (0.5, 0.9, 1.0):
             hits = rng.random(len(tn)) < p
             assert walk_links(ln, len(tn), hits, order) == walk_threaded(tn, hits)
+
+
+# ---- box pre-test nodes (option box_vnodes, round 5) -------------------------------------------
+PRETESTED = 8
+
+
+def vnode_links(bvh_bytes, vbox):
+    L = rtamd.amd()
+    bvh = ctypes.create_string_buffer(bvh_bytes, len(bvh_bytes))
+    vb = np.ascontiguousarray(vbox, np.float32)
+    n, nn = ctypes.c_int(), ctypes.c_int()
+    fp = vb.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    assert L.rt_debug_link_nodes_vbox(bvh, len(bvh_bytes), fp, len(vb) // 6, None, 0, ctypes.byref(n),
+                                      ctypes.byref(nn)) == 0
+    out = np.zeros((max(n.value, 1), 4), np.float32)
+    assert L.rt_debug_link_nodes_vbox(bvh, len(bvh_bytes), fp, len(vb) // 6, out.ctypes.data, out.nbytes,
+                                      ctypes.byref(n), ctypes.byref(nn)) == 0
+    return out[:n.value], nn.value
+
+
+def walk_links_n(ln, n_all, hits_of_slot):
+    """The kernel's loop over links with n_all nodes; hits_of_slot[address // 32] -> bool."""
+    words = ln.view(np.uint32)
+    leaves = words[2 * n_all:].reshape(-1, 2)
+    nx, tested = 0, []
+    while True:
+        while nx < LEAF:
+            nx = int(words[2 * (nx // 32) + 1, 2] if hits_of_slot[nx // 32] else words[2 * (nx // 32) + 1, 3])
+        if nx == LEND:
+            break
+        lf = leaves[nx & 0x7FFFFFFF]
+        tested.append((int(lf[0]) & 0xFF, int(lf[1])))
+        nx = int(lf[0]) >> 8
+        if nx == NEXT_END:
+            break
+    return tested
+
+
+@pytest.mark.parametrize("sid", [8, 7, 6, 4])
+def test_box_pretest_nodes_replay_the_walk(sid):
+    """The walk over the links with box pre-test nodes tests, under any pattern of box hits, the
+    threaded walk's prims in the same order, except that a box whose pre-test node misses is
+    skipped -- exactly what the leaf stage's pre-test did -- and each box of an all-box leaf is its
+    own record, marked pre-tested.  Other leaves are unchanged."""
+    scene = rtamd.Scene(sid, 64, 36, seed=1)
+    tn = threaded(scene)
+    n = len(tn)
+    nb = len(scene.buffers[4]) // 480
+    vbox = np.random.default_rng(sid).random(6 * max(nb, 1)).astype(np.float32)[:6 * nb]
+    ln, n_all = vnode_links(scene.buffers[1], vbox)
+    plain = links_of(scene.buffers[1])
+    order = check_layout(tn, plain)
+    # the tree's nodes keep their boxes and places; chain nodes follow, one per box of an all-box leaf,
+    # in threaded order, holding that box's bounds
+    assert np.array_equal(ln[:2 * n].reshape(n, 8)[:, :6].view(np.uint32), plain[:2 * n].reshape(n, 8)[:, :6].view(np.uint32))
+    chain = []
+    for k, nd in enumerate(tn):
+        t0, t1 = (int(nd["meta"]) >> 16) & 0xF, (int(nd["meta"]) >> 20) & 0xF
+        if is_leaf(nd) and t0 == 4 and t1 in (0, 4):
+            chain += [(k, int(nd["prims"]) & 0xFFFF)] + ([(k, int(nd["prims"]) >> 16)] if t1 else [])
+    assert n_all == n + len(chain)
+    for j, (_, b) in enumerate(chain):
+        assert np.array_equal(ln[2 * (n + j)][:4], vbox[6 * b:6 * b + 4]) and np.array_equal(ln[2 * (n + j) + 1][:2],
+                                                                                           vbox[6 * b + 4:6 * b + 6])
+    first = {}
+    for j, (k, _) in enumerate(chain):
+        first.setdefault(k, n + j)
+    pos = np.empty(n, np.int64)
+    pos[order] = np.arange(n)
+    rng = np.random.default_rng(100 + sid)
+    for p in (0.3, 0.7, 1.0):
+        for _ in range(20):
+            hits = rng.random(n) < p
+            vh = rng.random(max(len(chain), 1)) < 0.5
+            slot_hits = np.zeros(n_all, bool)
+            slot_hits[pos] = hits
+            slot_hits[n:] = vh[:len(chain)]
+            want = []
+            for types, prims in walk_threaded(tn, hits)[1]:
+                k = None
+                if types & 0xF == 4 and (types >> 4) in (0, 4):
+                    k = next(kk for kk in first if int(tn[kk]["prims"]) == prims and is_leaf(tn[kk]))
+                if k is None:
+                    want.append((types, prims))
+                    continue
+                boxes = [prims & 0xFFFF] + ([prims >> 16] if types >> 4 else [])
+                for j, b in enumerate(boxes):
+                    if slot_hits[first[k] + j]:
+                        want.append((4 | PRETESTED, b))
+            assert walk_links_n(ln, n_all, slot_hits) == want
