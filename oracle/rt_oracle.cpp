@@ -108,7 +108,13 @@ float rand(Inv& I) {
     co.y += I.rand_factor;
     v2 k = {12.9898f, 78.233f};
     if (I.C) I.C->c.rand_calls++;
+#ifdef RT_PROBE_SIN_F64
+    // probe build only (tools/scene8_residual_probe.py): the hash's sin as a
+    // correctly rounded float of the double sine, instead of the shipped g_sin
+    return g_fract((float)std::sin((double)g_dot2(co, k)) * 43758.5453123f);
+#else
     return g_fract(g_sin(g_dot2(co, k)) * 43758.5453123f);
+#endif
 }
 float rand(Inv& I, float mn, float mx) { return mn + rand(I) * (mx - mn); }          // :10-12
 int rand_int(Inv& I, int mn, int mx) { return rt_f2i(floorf(rand(I, (float)mn, (float)(mx + 1)))); }  // :15-17
@@ -728,7 +734,19 @@ v3 ray_color(Inv& I, Ray ray) {   // :298-343
             acc = mul3(acc, I.attenuation);
             continue;
         }
+#if defined(RT_PROBE_Q1)
+        // probe builds only (tools/scene8_residual_probe.py): other readings of SURVEY App. A Q1 (no
+        // registered light: lights_random's missing return).  1: the direction is left unchanged
+        // (the rand() for the branch is still drawn); 2: only an isotropic (fog) scatter keeps its
+        // direction, a Lambertian one takes the zero direction as shipped
+        if (rand(I) < 0.5f) {
+            const bool keep = I.S->lights_count <= 0 &&
+                              (RT_PROBE_Q1 == 1 || ((I.material >> 16) & 0xFFFF) == RT_MAT_ISOTROPIC);
+            if (!keep) ray.dir = lights_random(I, ray.o);
+        }
+#else
         if (rand(I) < 0.5f) ray.dir = lights_random(I, ray.o);
+#endif
         float lpdf = lights_pdf_value(I, ray.o, ray.dir);
         float pdf_value = 0.5f * lpdf + 0.5f * material_pdf_value(ray.dir, I.material, rec.normal);
         if (pdf_value == 0.0f) {
