@@ -194,6 +194,13 @@ struct rt_kernel_args {
 enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
        RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_LEAF_PF, RT_LI_SHADE_LDS, RT_LI_WALK_FRAC, RT_LI_BVH_MODE, RT_LI_VNODES, RT_LI_N = 20 };
 
+#ifdef RT_AB_KNOBS
+// A/B library only (rt_kernel_variants.hip): the structures the release library does not ship
+#define RT_FAST_STACK 16   // the near-first walk's per-lane stack (shorts in LDS)
+enum { RT_AB_SHAPE_FAST_LDS = 0, RT_AB_SHAPE_FAST_GLOBAL, RT_AB_SHAPE_LINK_PIXEL, RT_AB_SHAPE_META_LDS,
+       RT_AB_SHAPE_META_GLOBAL };
+int rt_launch_render_ab(int shape, rt_kernel_args& a, const rt_kernel_args* d, size_t lds, bool stats, void* stream);
+#endif
 // launcher implemented in rt_kernel.hip
 int rt_resident_waves(void);   // waves a render launch keeps resident on the current device (its grid, at most)
 // sets a.acc_lds; info (may be NULL): RT_LI_* of the launch

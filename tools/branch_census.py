@@ -24,7 +24,7 @@ def main():
                     "-fno-slp-vectorize", "-gline-tables-only", "-I" + ROOT + "/include", "-I" + PKG + "/csrc",
                     "--cuda-device-only", "-S", "-o", asm, PKG + "/csrc/rt_kernel.hip"], check=True,
                    capture_output=True)
-    head = re.compile(r"_ZN12_GLOBAL__N_117render_persistentILb1ELi4ELb0ELb1ELi%dELb0ELi%dEEEvPK14rt_kernel_args:"
+    head = re.compile(r"_ZN12_GLOBAL__N_117render_persistentILi4ELb0ELi%dELi%dEEEvPK14rt_kernel_args:"
                       % (a.block, a.opt))
     files, cur, inside = {}, None, False
     hist = collections.Counter()

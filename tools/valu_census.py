@@ -11,7 +11,8 @@ import subprocess
 
 ROOT = __file__.rsplit("/tools/", 1)[0]
 PKG = ROOT + "/raytracing-book_amd"
-SRC = {"rt_kernel.hip": PKG + "/csrc/rt_kernel.hip", "rt_glsl.h": ROOT + "/include/rt/rt_glsl.h"}
+SRC = {"rt_kernel.hip": PKG + "/csrc/rt_kernel.hip", "rt_kernel_common.h": PKG + "/csrc/rt_kernel_common.h",
+       "rt_glsl.h": ROOT + "/include/rt/rt_glsl.h"}
 DEF = re.compile(r"^(?:template\s*<[^>]*>\s*)?(?:__device__|__global__|RT_HD|__host__)[^(;]*?\b(\w+)\s*\(")
 
 
@@ -38,7 +39,7 @@ def main():
                     "--cuda-device-only", "-S", "-o", asm, PKG + "/csrc/rt_kernel.hip"], check=True,
                    capture_output=True)
     fmap = {k: function_of_lines(v) for k, v in SRC.items()}
-    head = re.compile(r"_ZN12_GLOBAL__N_117render_persistentILb1ELi4ELb0ELb1ELi%dELb0ELi%dEEEvPK14rt_kernel_args:"
+    head = re.compile(r"_ZN12_GLOBAL__N_117render_persistentILi4ELb0ELi%dELi%dEEEvPK14rt_kernel_args:"
                       % (a.block, a.opt))
     files, loc, inside = {}, ("?", 0), False
     per_fn, per_line = collections.Counter(), collections.Counter()
