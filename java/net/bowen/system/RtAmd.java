@@ -75,6 +75,7 @@ public final class RtAmd implements AutoCloseable {
     private static final MethodHandle SET_PARTITION =
             fn("rt_set_partition", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, JAVA_INT));
     private static final MethodHandle RESIZE = fn("rt_resize", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT));
+    private static final MethodHandle SET_BVH_MODE = fn("rt_set_bvh_mode", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT));
     private static final MethodHandle RENDER = fn("rt_render", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, ADDRESS));
     private static final MethodHandle SYNC = fn("rt_sync", FunctionDescriptor.of(JAVA_INT, ADDRESS));
     private static final MethodHandle READ_IMAGE = fn("rt_read_image", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
@@ -172,6 +173,14 @@ public final class RtAmd implements AutoCloseable {
     }
 
     /** One process per GPU: this process renders the stripes s with s % world == rank. */
+    /** rt_set_bvh_mode: RT_BVH_REFERENCE (0, the default, bit-exact) or RT_BVH_SAH (1, the non-parity
+     *  fast mode: a binned-SAH tree over the same prims; statistically equal images, not bit-exact). */
+    public static final int BVH_REFERENCE = 0, BVH_SAH = 1;
+
+    public void setBvhMode(int mode) {
+        check(call(() -> (int) SET_BVH_MODE.invokeExact(ctx, mode)), ctx);
+    }
+
     public void setPartition(int rank, int world, int stripeRows) {
         check(call(() -> (int) SET_PARTITION.invokeExact(ctx, rank, world, stripeRows)), ctx);
         this.rank = rank;
