@@ -1814,7 +1814,9 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         const size_t media_f4 = (n_med > 0 && n_med <= 64) ? 3 * (size_t)n_med : 0;
         const size_t sph_f4 = (c->sph_lds && pooled) ? 2 * (size_t)n_sph : 0;
         const size_t box_f4 = (size_t)RT_BOXC_F4 * n_box;   // every box's record (bounds; compact faces)
-        const size_t cap_s = RT_LDS_DYN_BYTES / 16, cap_b = RT_LDS_BIG_BYTES / 16;
+        const bool stats_twin = c->variant == 39;   // static LDS counters beside the dynamic region
+        const size_t cap_s = RT_LDS_DYN_BYTES / 16,
+                     cap_b = (stats_twin ? RT_LDS_BIG_STATS_BYTES : RT_LDS_BIG_BYTES) / 16;
         const size_t ess = node_f4 + leaf_f4 + perlin_f4 + media_f4;   // what every walk and shade reads
         const size_t all = ess + sph_f4 + box_f4;
         const size_t node_cap = c->lds_node_cap > 0 ? (size_t)c->lds_node_cap / 32 * 2 : node_f4;

@@ -40,8 +40,11 @@
 #define RT_LDS_DYN_BYTES (80 * 1024 - RT_LDS_ACC_BYTES)   // link nodes + Perlin + media, or variant 61's tree + stacks
 // the pooled link-walk kernel as one 1024-thread workgroup per CU (16 waves, 4 per SIMD, the
 // same as two workgroups of 512): one copy of the nodes per CU leaves room for the leaf
-// tests' sphere and box records; 8 KB of the 160 KB stay for the stats build's static counters
-#define RT_LDS_BIG_BYTES (152 * 1024)
+// tests' sphere and box records.  The release kernels have no static LDS and take all 160 KB; the
+// stats twins (A/B library) keep 8 KB for their static counters (RT_LDS_BIG_STATS_BYTES), so their
+// plan may leave out the last table (rt_capi.hip: the LDS plan by variant)
+#define RT_LDS_BIG_BYTES (160 * 1024)
+#define RT_LDS_BIG_STATS_BYTES (152 * 1024)
 #define RT_LDS_NODE_BYTES (64 * 1024)   // threaded (meta-word) nodes in LDS when they fit
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
