@@ -279,9 +279,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             const bool dir_zero = (S.d.x == 0.0f) && (S.d.y == 0.0f) && (S.d.z == 0.0f);
             status = (dir_zero || P.n_nodes == 0) ? RT_SM_HIT : RT_SM_TRACE;
             if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);
-        }
-        // per-ray constants of every walk (new or resumed: the same values again)
-        if (status == RT_SM_TRACE) {
+            // the walk's per-ray constants, kept while it runs (a resumed walk has them)
             inv = mk3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
             a = g_dot(S.d, S.d);
         }

@@ -73,7 +73,7 @@ def test_shading_tables_match_oracle(gpu, scene_id, w, h, frames, depth, shade):
     """The shading tables in LDS (option shade_lds, default on: sphere records' third float4,
     compact boxes' materials with their face normals rebuilt from the compact record, texture
     descriptors and the small texture slots) and the records read from global memory (off):
-    every scene bit for bit against the oracle; scene 8 stages the tables that fit (asserted)."""
+    every scene bit for bit against the oracle; scene 8 stages all three tables (asserted)."""
     s = rtamd.Scene(scene_id, w, h, seed=1)
     ref = oracle_image(s, frames, max_depth=depth)
     ctx = rtamd.RenderContext(options={"shade_lds": shade})
@@ -84,9 +84,8 @@ def test_shading_tables_match_oracle(gpu, scene_id, w, h, frames, depth, shade):
     out, info = ctx.read_image(), ctx.last_launch()
     ctx.close()
     if scene_id == 8 or not shade:
-        # scene 8 stages all three tables; with the box pre-test nodes in LDS (option box_vnodes, the
-        # default) the boxes' material table no longer fits beside them (sphere materials and textures do)
-        assert info["shade_lds"] == (7 if info["box_vnodes"] == 0 else 5) * shade, info
+        # scene 8 stages all three tables (beside the box pre-test nodes: the release kernels' 160 KB)
+        assert info["shade_lds"] == 7 * shade, info
     assert bit_equal(out, ref), f"shade_lds {info['shade_lds']}: {mismatch_report(out, ref)}"
 
 

@@ -8,6 +8,8 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/raytracing-book_amd
 TMP=$(mktemp -d)
 git -C "$ROOT" show "$REV:raytracing-book_amd/csrc/rt_kernel.hip" > "$TMP/rt_kernel.hip"
+# the shared device code (round 5 on): found beside the kernel source before the working tree's
+git -C "$ROOT" show "$REV:raytracing-book_amd/csrc/rt_kernel_common.h" > "$TMP/rt_kernel_common.h" 2>/dev/null || rm -f "$TMP/rt_kernel_common.h"
 # the built-in definitions (rt_glsl.h) of that revision too: searched before the working tree's
 mkdir -p "$TMP/include/rt"
 git -C "$ROOT" show "$REV:include/rt/rt_glsl.h" > "$TMP/include/rt/rt_glsl.h"
