@@ -97,3 +97,24 @@ def test_sah_mode_statistics_match_the_reference_bvh(gpu, sid):
           f"p99 {np.quantile(rel, 0.99):.4f} mean {rel.mean():.4f} over {ok.sum()} block-channels")
     assert np.all(g < 0.005), g
     assert rel.max() < BLOCK_TOL[sid], rel.max()
+
+
+def test_sah_mode_partitions_render_the_same_bits(gpu):
+    """The fast mode in a multi-process partition (rt_set_partition): every rank builds the same SAH
+    tree from the same upload (the builder is deterministic), so the stripes of 3 ranks equal the
+    one-context image bit for bit -- the weak-scaling bench's N-rank fast-mode line is the 1-GPU
+    image cut into stripes."""
+    sc = rtamd.Scene(8, 64, 40, seed=1)
+    full, _, _ = render(sc, 4, "sah")
+    world, stripe = 3, 8
+    for rank in range(world):
+        ctx = rtamd.RenderContext(devices=(0,), rank=rank, world=world, stripe_rows=stripe)
+        ctx.set_bvh_mode("sah")
+        ctx.upload_scene(sc)
+        ctx.set_params(max_depth=5, spp=4)
+        ctx.resize(64, 40)
+        ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+        part = ctx.read_image()
+        ctx.close()
+        rows = rtamd.stripe_rows_of(40, rank, world, stripe)
+        assert bit_equal(part[:len(rows)], full[rows]), rank
