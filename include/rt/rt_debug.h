@@ -109,7 +109,8 @@ enum {
     RT_OPTION_SPARSE_STAGE = 18,        /* staged chunks write only colours that are not
                                            exactly zero, plus a flag byte per sample (1)    */
     RT_OPTION_SPHERE_PAIRS = 19,        /* kernels testing a two-sphere leaf's spheres at
-                                           once, when most leaves are such pairs (1)        */
+                                           once, when most leaves are such pairs (1); 2:
+                                           always, compact-box kernels included            */
     RT_OPTION_LEAF_PREFETCH = 20,       /* compact-box kernels: each leaf slot's record loaded
                                            before the prim-type blocks when spheres, boxes
                                            and media are all staged in LDS (1)              */

@@ -199,7 +199,8 @@ struct rt_ctx {
     bool tl_leaf_lds = true;     // two-level walk: the leaf records in LDS beside the top levels (when they fit)
     int perlin_pk_slot = -1;     // texture slot whose Perlin table has its packed copy (Device::perlin_pk)
     bool sparse_stage = true;    // staged chunks store only the colours that are not exactly zero (option)
-    bool sphere_pairs = true;    // the sphere-pair kernels when most leaves hold two spheres (option)
+    int sphere_pairs = 1;        // the sphere-pair kernels when most leaves hold two spheres (option; 2: always,
+                                 // compact-box kernels included)
     int pair_leaves = -1;        // per mille of the link-format leaves that hold two spheres (< 0: not counted)
     bool perlin_pk = true;       // stage the packed Perlin table (option; else the texture as uploaded)
     int n_boxc_ok = 0;           // boxes whose compact record reproduces their faces
@@ -1801,7 +1802,8 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     // the sphere-pair kernels (rt_kernel.hip leaf_prims_t SPAIR) for a BVH whose leaves are mostly
     // two spheres (scene 0: 485 spheres); measured slower where they are not
     if (c->pair_leaves < 0) c->pair_leaves = pair_leaves_permille(c->walk_links, c->n_walk_nodes);
-    a.sph_pairs = (c->sphere_pairs && c->pair_leaves >= 500) ? 1 : 0;
+    // option sphere_pairs = 2: the pair kernels whatever the share, compact-box kernels included
+    a.sph_pairs = c->sphere_pairs == 2 ? 2 : (c->sphere_pairs && c->pair_leaves >= 500) ? 1 : 0;
     a.perlin_slot = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
@@ -2430,7 +2432,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_TL_LEAF_LDS: c->tl_leaf_lds = v != 0; break;
         case RT_OPTION_PERLIN_PACKED: c->perlin_pk = v != 0; break;
         case RT_OPTION_SPARSE_STAGE: c->sparse_stage = v != 0; break;
-        case RT_OPTION_SPHERE_PAIRS: c->sphere_pairs = v != 0; break;
+        case RT_OPTION_SPHERE_PAIRS: if (v < 0 || v > 2) return bad(); c->sphere_pairs = v; break;
         case RT_OPTION_LEAF_PREFETCH: c->leaf_prefetch = v != 0; break;
         case RT_OPTION_TL_SMALL_LDS: c->tl_small_lds = v != 0; break;
         case RT_OPTION_SHADE_LDS: c->shade_lds = v != 0; break;

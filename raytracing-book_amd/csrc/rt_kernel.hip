@@ -567,7 +567,8 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         info[RT_LI_CHUNKS] = a.n_chunks;
         info[RT_LI_SPINE] = pool ? a.spine_len : 0;
         info[RT_LI_SPARSE] = a.samples && a.sflags ? 1 : 0;
-        info[RT_LI_SPAIR] = (pool && shape == LINK_LDS && a.sph_pairs && !a.box_all_cmp && a.sph_lds >= 0) ? 1 : 0;
+        info[RT_LI_SPAIR] = (pool && shape == LINK_LDS && a.sph_lds >= 0 &&
+                             ((a.sph_pairs && !a.box_all_cmp) || (a.sph_pairs == 2 && a.fastdiv))) ? 1 : 0;
         info[RT_LI_LEAF_PF] = (pool && (shape == LINK_LDS || shape == LINK_TL)) ? a.leaf_pf : 0;
         info[RT_LI_WALK_FRAC] = a.walk_frac;
         info[RT_LI_SHADE_LDS] = (a.sph_mat_lds >= 0) + 2 * (a.box_mat_lds >= 0) + 4 * (a.tex_lds >= 0);
@@ -601,7 +602,8 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
                : (a.box_all_cmp ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_BOXC) : RT_KERNEL(BLOCK, (OPT))))
     // ... and, for a scene whose leaves are mostly sphere pairs (a.sph_pairs), without compact boxes
 #define RT_LINK4S(BLOCK, OPT)                                                                                 \
-    ((a.sph_pairs && !a.box_all_cmp)                                                                         \
+    ((a.sph_pairs == 2 && a.box_all_cmp && a.fastdiv) ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_BOXC | RT_OPT_SPAIR) : \
+    (a.sph_pairs && !a.box_all_cmp)                                                                          \
          ? (a.fastdiv ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_SPAIR) : RT_KERNEL(BLOCK, (OPT) | RT_OPT_SPAIR)) \
          : RT_LINK4(BLOCK, OPT))
     switch (shape) {

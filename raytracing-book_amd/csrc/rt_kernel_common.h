@@ -600,6 +600,9 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             pretested = (ty & RT_LINK_PRETESTED) != 0;
             ty &= 7;
         }
+        // the second slot is empty in every lane of the wave (singleton leaves, the pre-tested boxes'
+        // records): nothing to test, its record loads skipped (wave-uniform)
+        if (BOXC && s == 1 && __ballot(ty != 0) == 0) break;
         if (STATS) {
             st_pred(st, ty == RT_MODEL_SPHERE, ST_SPH_IT, ST_SPH_LN);
             st_pred(st, ty == RT_MODEL_QUAD, ST_QUAD_IT, ST_QUAD_LN);
