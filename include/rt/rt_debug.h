@@ -124,6 +124,9 @@ enum {
     RT_OPTION_BOX_VNODES = 23,          /* compact-box kernels: each all-box leaf's box bounds
                                            pre-tests as nodes of the walk, the leaf stage
                                            testing only the boxes they pass (1)            */
+    RT_OPTION_ZERO_DIR_END = 24,        /* a path whose next direction is vec3(0) (the no-
+                                           light branch) ends in its shading pass with the
+                                           miss colour its next bounce would give (1)       */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

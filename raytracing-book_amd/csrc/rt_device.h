@@ -127,6 +127,8 @@ struct rt_kernel_args {
     int walk_frac;               // render_sm: a round's node walk stops once this many 64ths of its lanes
                                  // hold a leaf or ended (64: all of them)
     int box_vnodes;              // the links carry box pre-test nodes (leaf records marked RT_LINK_PRETESTED)
+    int zero_dir_end;            // render_stream: a path whose next direction is vec3(0) ends with its miss
+                                 // colour in the same shading pass (option zero_dir_end)
     int leaf_pf;                 // BOXC kernels: the leaf stage prefetches each slot's record (spheres, boxes
                                  // and media all staged in LDS; rt_kernel.hip leaf_prims_t)
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)

@@ -337,6 +337,13 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             if (!done && S.depth >= P.max_depth) {   // the loop is exhausted: final_color stays vec3(0)
                 cur3 = mk3s(0.0f);
                 done = true;
+            } else if (!done && P.zero_dir_end && S.d.x == 0.0f && S.d.y == 0.0f && S.d.z == 0.0f) {
+                // a zero direction (the no-light mixture branch, SURVEY App. A Q1: an isotropic
+                // scatter goes on along vec3(0)): the next bounce hits nothing and draws no rand()
+                // (bounce(), compute.glsl:226-229, 308-309), so its miss colour -- acc x background
+                // with the acc of now -- is the path's colour; taken here instead of one more pass
+                cur3 = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
+                done = true;
             }
             if (done) {
                 const float4 c4 = make_float4(cur3.x, cur3.y, cur3.z, 0.0f);
