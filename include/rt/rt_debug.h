@@ -127,9 +127,6 @@ enum {
     RT_OPTION_ZERO_DIR_END = 24,        /* a path whose next direction is vec3(0) (the no-
                                            light branch) ends in its shading pass with the
                                            miss colour its next bounce would give (1)       */
-    RT_OPTION_SPEC_WALK = 25,           /* a lane whose walk reached a leaf walks on past it
-                                           while the wave's other lanes walk, the progress
-                                           kept when the leaf's tests leave ray_t.max (0)   */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

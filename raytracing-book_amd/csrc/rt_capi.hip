@@ -152,7 +152,6 @@ struct rt_ctx {
     std::vector<float4> boxc_host;  // the compact box records (host copy of Device::dboxc)
     bool box_vnodes = true;         // option box_vnodes
     bool zero_dir_end = true;       // option zero_dir_end (rt_kernel.hip render_stream)
-    bool spec_walk = false;         // option spec_walk (rt_kernel.hip render_stream)
     FastTables fast;
     std::vector<float4> links;   // build_links(dnodes), empty when unavailable
     int fast_gen = 0;
@@ -1730,7 +1729,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                     : 0;
     a.variant = c->variant;
     a.zero_dir_end = c->zero_dir_end ? 1 : 0;
-    a.spec_walk = c->spec_walk ? 1 : 0;
     a.sm_batch = c->sm_batch;
     a.walk_frac = c->walk_frac ? c->walk_frac : walk_frac_for(c->n_link_nodes);   // by the tree, not the pre-test nodes
     const FastTables& F = c->fast;
@@ -2442,7 +2440,6 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SHADE_LDS: c->shade_lds = v != 0; break;
         case RT_OPTION_BOX_VNODES: c->box_vnodes = v != 0; break;
         case RT_OPTION_ZERO_DIR_END: c->zero_dir_end = v != 0; break;
-        case RT_OPTION_SPEC_WALK: c->spec_walk = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2482,7 +2479,6 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_SHADE_LDS: *v = c->shade_lds; break;
         case RT_OPTION_BOX_VNODES: *v = c->box_vnodes; break;
         case RT_OPTION_ZERO_DIR_END: *v = c->zero_dir_end; break;
-        case RT_OPTION_SPEC_WALK: *v = c->spec_walk; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

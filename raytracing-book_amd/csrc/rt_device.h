@@ -129,7 +129,6 @@ struct rt_kernel_args {
     int box_vnodes;              // the links carry box pre-test nodes (leaf records marked RT_LINK_PRETESTED)
     int zero_dir_end;            // render_stream: a path whose next direction is vec3(0) ends with its miss
                                  // colour in the same shading pass (option zero_dir_end)
-    int spec_walk;               // render_stream: speculative walk past a pending leaf (option spec_walk)
     int leaf_pf;                 // BOXC kernels: the leaf stage prefetches each slot's record (spheres, boxes
                                  // and media all staged in LDS; rt_kernel.hip leaf_prims_t)
     int debug_flags;             // ablation switches for attribution runs (RT_DEBUG_FLAGS; 0 = exact)

@@ -96,7 +96,6 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                                               unsigned long long* st) {
     constexpr bool TL = (OPT & RT_OPT_TL) != 0;
     constexpr bool BOXC = (OPT & RT_OPT_BOXC) != 0;
-    constexpr bool SPEC = (OPT & RT_OPT_SPEC) != 0 && !TL;
     const int lane = threadIdx.x & 63;
     const bool staged = P.samples != nullptr;
     const int tiles_x = (P.width + 7) >> 3;
@@ -133,7 +132,6 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     float tmax = RT_INFINITY, a = 0.0f;
     v3 inv = mk3s(0.0f);
     uint32_t nx = RT_LINK_END;
-    uint32_t pend = RT_LINK_END;   // SPEC: the pending leaf (link_walk_spec), RT_LINK_END = none
     int status = RT_SM_FRESH;
     // a progress watchdog: on its first pass and every 256th, a wave that has stored no
     // sample since the previous check more than P.watchdog_ticks ago (120 s by default)
@@ -278,7 +276,6 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             has = false;
             tmax = RT_INFINITY;
             nx = spine_entry(P, S.o, S.d);
-            pend = RT_LINK_END;
             const bool dir_zero = (S.d.x == 0.0f) && (S.d.y == 0.0f) && (S.d.z == 0.0f);
             status = (dir_zero || P.n_nodes == 0) ? RT_SM_HIT : RT_SM_TRACE;
             if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);
@@ -301,11 +298,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             if (status == RT_SM_TRACE) {
                 if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
                 unsigned long long t0 = STATS ? clock64() : 0;
-                if (SPEC) {
-                    const int needw = (__popcll(__ballot(1)) * P.walk_frac + 63) >> 6;
-                    nx = wave_exact ? link_walk_spec<true, STATS>(ns, leaves, nx, pend, S.o, inv, 0.001f, tmax, needw, st)
-                                    : link_walk_spec<false, STATS>(ns, leaves, nx, pend, S.o, inv, 0.001f, tmax, needw, st);
-                } else if (P.walk_frac >= 64) {
+                if (P.walk_frac >= 64) {
                     nx = wave_exact ? link_walk<true, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, st)
                                     : link_walk<false, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, st);
                 } else {
@@ -314,28 +307,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                                     : link_walk_part<false, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, needw, st);
                 }
                 if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);
-                if (SPEC) {
-                    // the leaf to test: the pending one, else the one the walk stopped at
-                    const uint32_t lx = pend != RT_LINK_END ? pend : nx;
-                    if (lx == RT_LINK_END) {
-                        status = RT_SM_HIT;
-                    } else if ((int)lx < 0) {
-                        unsigned long long t1 = STATS ? clock64() : 0;
-                        if (STATS) st_lanes(st, ST_LEAF_IT, ST_LEAF_LN);
-                        const uint2 lf = leaves[lx & 0x7FFFFFFFu];
-                        const float tm0 = tmax;
-                        leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0>(P, lf.x << 16, lf.y, S.o, S.d, inv, a,
-                                                                                 S.time, 0.001f, tmax, S.rf, fx, fy,
-                                                                                 h, has, st);
-                        if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
-                        const uint32_t sk = lf.x >> 8;
-                        // no pending leaf (nx was the leaf), or its tests moved ray_t.max: on from the
-                        // skip node; otherwise the speculative walk's position stands
-                        if (pend == RT_LINK_END || tmax != tm0) nx = sk == RT_LINK_NEXT_END ? RT_LINK_END : sk;
-                        pend = RT_LINK_END;
-                        if (nx == RT_LINK_END) status = RT_SM_HIT;
-                    }
-                } else if ((int)nx >= 0) {
+                if ((int)nx >= 0) {
                     // still walking: the next round goes on from nx
                 } else if (nx == RT_LINK_END) {
                     status = RT_SM_HIT;
@@ -622,7 +594,6 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
         return -1;
 
     constexpr int SM = RT_OPT_POOL | RT_OPT_SM | RT_OPT_STREAM;
-    constexpr int SMS = SM | RT_OPT_SPEC;
     // the instantiations: <MINW, STATS, BLOCK, OPT> (stats twins in the A/B build only)
 #ifdef RT_AB_KNOBS
 #define RT_KERNEL(BLOCK, OPT)                                                                            \
@@ -649,9 +620,9 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
                 rc = rt_launch_render_ab(RT_AB_SHAPE_LINK_PIXEL, a, d, lds, stats, st);
 #endif
             } else if (a.block == 1024) {
-                rc = a.spec_walk ? RT_LINK4S(1024, SMS) : RT_LINK4S(1024, SM);
+                rc = RT_LINK4S(1024, SM);
             } else {
-                rc = a.spec_walk ? RT_LINK4S(512, SMS) : RT_LINK4S(512, SM);
+                rc = RT_LINK4S(512, SM);
             }
             break;
         case LINK_TL: rc = RT_LINK4(1024, SM | RT_OPT_TL); break;

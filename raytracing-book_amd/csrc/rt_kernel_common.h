@@ -29,7 +29,6 @@ typedef rt_kernel_args KP;
 #define RT_OPT_TL 16    // with RT_OPT_STREAM: two-level walk (top levels in LDS, the rest of the nodes global)
 #define RT_OPT_BOXC 32  // with RT_OPT_STREAM: every box has a compact record (box_test_compact), no full box test
 #define RT_OPT_SPAIR 64 // with RT_OPT_STREAM: leaves of two spheres tested at once (leaf_prims_t; most leaves are)
-#define RT_OPT_SPEC 128 // with RT_OPT_STREAM, not RT_OPT_TL: the walk goes on past a pending leaf (link_walk_spec)
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -793,55 +792,6 @@ __device__ __forceinline__ uint32_t link_walk_part(const NodeSrc& ns, uint32_t n
         }
         const unsigned long long walking = __ballot((int)nx >= 0);
         if (walking == 0 || __popcll(__ballot(1) & ~walking) >= need) break;
-    }
-    return nx;
-}
-
-// link_walk_part with a pending leaf per lane (RT_OPT_SPEC, option spec_walk).  A lane that
-// reaches a leaf while it holds none makes it its pending leaf `pend` and walks on from the
-// leaf's skip node, under the ray_t.max of now; a lane that holds one stops at its next leaf.
-// Walking on is speculative: the reference tests the pending leaf first, and its tests may
-// shrink ray_t.max, after which the walk from the skip node is a different one.  If they do not,
-// the nodes walked meanwhile are exactly the reference's (every node test depends only on the
-// node, the ray and ray_t), so render_stream keeps the progress; if they do, it restarts at the
-// skip node -- either way each lane's leaves are tested in the reference's order under the
-// reference's ray_t, with its medium draws in that order.  So the lanes that reach a leaf early
-// walk on while the wave's last walkers finish, instead of idling.  The round ends once `need`
-// lanes hold a leaf to test (pending, or stopped at one) or have ended, or none walks.
-template <bool EXACT, bool STATS>
-__device__ __forceinline__ uint32_t link_walk_spec(const NodeSrc& ns, const uint2* __restrict__ leaves, uint32_t nx,
-                                                   uint32_t& pend, v3 o, v3 inv, float tmin, float tmax, int need,
-                                                   unsigned long long* st) {
-    for (;;) {
-        if ((int)nx < 0 && nx != RT_LINK_END && pend == RT_LINK_END) {   // a leaf reached: pending, walk on
-            pend = nx;
-            const uint32_t s = leaves[nx & 0x7FFFFFFFu].x >> 8;
-            nx = s == RT_LINK_NEXT_END ? RT_LINK_END : s;
-        }
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            if ((int)nx >= 0) {
-                if (STATS) {
-                    st_lanes(st, ST_NODE_IT, ST_NODE_LN);
-                    st_small(st, true, ST_NODE_SM);
-                }
-                float4 n0, n1;
-                load_node<STATS, false>(ns, nx, n0, n1);
-                bool hit;
-                if (!EXACT) {
-                    hit = aabb_pk(n0, n1, o, inv, tmin, tmax);
-                } else {
-                    float lo = tmin, hi = tmax;
-                    slab(n0.x, n0.y, o.x, inv.x, lo, hi);
-                    slab(n0.z, n0.w, o.y, inv.y, lo, hi);
-                    slab(n1.x, n1.y, o.z, inv.z, lo, hi);
-                    hit = !(hi <= lo);
-                }
-                nx = __float_as_uint(hit ? n1.z : n1.w);
-            }
-        }
-        const unsigned long long walking = __ballot((int)nx >= 0);
-        if (walking == 0 || __popcll(__ballot(pend != RT_LINK_END || (int)nx < 0)) >= need) break;
     }
     return nx;
 }
