@@ -1252,42 +1252,9 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         return true;
     }
     float& rf = S.rf;
-    // The scatter's first rand() draws, one loop for every material of the wave: Lambertian's r1, r2;
-    // random_unit_vector's rejection loop (random.glsl:40-49) for metal (its only draws; the reflect
-    // and normalize before it draw none) and isotropic; the dielectric's reflectance draw when it does
-    // not reflect totally.  Each lane draws what its material's code draws, in that order (rnd() reads
-    // only rf, which advances per draw), so the same values; the wave runs the draws of all its
-    // materials once instead of one block (and one rejection loop) per material.
-    float eta = 0.0f, cos_t = 0.0f;
-    bool refl = false;
-    if (mid == RT_MAT_DIELECTRIC) {
-        float nior = (float)(material & 0xFFFF) / 65535.0f;
-        eta = g_mix(1.0f, 2.5f, nior);
-        if (front) eta = 1.0f / eta;
-        d = g_normalize(d);
-        cos_t = g_min(g_dot(neg3(d), normal), 1.0f);
-        float sin_t = sqrtf(1.0f - cos_t * cos_t);
-        refl = eta * sin_t > 1.0f;
-    }
-    const int nd = mid == RT_MAT_LAMBERTIAN ? 2
-                 : (mid == RT_MAT_METAL || mid == RT_MAT_ISOTROPIC) ? 3
-                 : (mid == RT_MAT_DIELECTRIC && !refl) ? 1 : 0;
-    float q0 = 0.0f, q1 = 0.0f, q2 = 0.0f;
-    v3 up = mk3s(0.0f);
-    for (bool go = nd > 0; go;) {
-        q0 = rnd(rf, px, py);
-        if (nd >= 2) q1 = rnd(rf, px, py);
-        go = false;
-        if (nd == 3) {
-            q2 = rnd(rf, px, py);
-            up = mk3(-1.0f + q0 * 2.0f, -1.0f + q1 * 2.0f, -1.0f + q2 * 2.0f);
-            go = !(g_dot(up, up) < 1.0f);
-        }
-    }
-    if (nd == 3) up = g_normalize(up);   // random_unit_vector()
     if (mid == RT_MAT_LAMBERTIAN) {
-        float r1 = q0;
-        float r2 = q1;
+        float r1 = rnd(rf, px, py);
+        float r2 = rnd(rf, px, py);
         float phi = 2.0f * RT_PI * r1;
         float s, c;
         g_sincos(phi, &s, &c);
@@ -1298,21 +1265,28 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         float fuzz = (float)(material & 0xFFFF) / 65535.0f;
         d = g_reflect(d, normal);
         v3 n = g_normalize(d);
-        d = add3(n, scale3(up, fuzz));
+        d = add3(n, scale3(rand_unit_vec(rf, px, py), fuzz));
         should = g_dot(d, normal) > 0.0f;
         skip_pdf = true;
     } else if (mid == RT_MAT_DIELECTRIC) {
+        float nior = (float)(material & 0xFFFF) / 65535.0f;
+        float eta = g_mix(1.0f, 2.5f, nior);
+        if (front) eta = 1.0f / eta;
+        d = g_normalize(d);
+        float cos_t = g_min(g_dot(neg3(d), normal), 1.0f);
+        float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        bool refl = eta * sin_t > 1.0f;
         if (!refl) {
             float r0 = (1.0f - eta) / (1.0f + eta);
             r0 = r0 * r0;
             float rr = r0 + (1.0f - r0) * g_pow5(1.0f - cos_t);
-            refl = rr > q0;
+            refl = rr > rnd(rf, px, py);
         }
         d = refl ? g_reflect(d, normal) : g_refract(d, normal, eta);
         should = true;
         skip_pdf = true;
     } else if (mid == RT_MAT_ISOTROPIC) {
-        d = up;
+        d = rand_unit_vec(rf, px, py);
         should = true;
     }
     if ((fabsf(d.x) < 1e-8f) && (fabsf(d.y) < 1e-8f) && (fabsf(d.z) < 1e-8f)) d = normal;
