@@ -153,19 +153,6 @@ __device__ __forceinline__ float div_nr(float num, float den, float r) {
     const float q1 = fmaf(fmaf(-den, q0, num), r, q0);
     return fmaf(fmaf(-den, q1, num), r, q1);
 }
-// Two quotients at once: the same operations on packed pairs (v_pk_mul_f32 / v_pk_fma_f32 round
-// each lane as v_mul_f32 / v_fma_f32 do; v_rcp_f32 has no packed form), so the same bits.
-typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2v rcp_nr2(f2v den) {
-    const f2v r0 = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-    return pk_fma(pk_fma(-den, r0, f2v{1.0f, 1.0f}), r0, r0);
-}
-__device__ __forceinline__ f2v div_nr2(f2v num, f2v den, f2v r) {
-    const f2v q0 = num * r;
-    const f2v q1 = pk_fma(pk_fma(-den, q0, num), r, q0);
-    return pk_fma(pk_fma(-den, q1, num), r, q1);
-}
 // Where the leaf tests use them (FD kernels, P.fastdiv: the camera and every record
 // within 2^20, faces' delta in [2^-60, 2^20]), every kept quotient is in that
 // regime: a box or quad plane divides by a denominator of at least 1e-8 (smaller
@@ -177,35 +164,19 @@ __device__ __forceinline__ f2v div_nr2(f2v num, f2v den, f2v r) {
 // ------------------------------------------------------------- primitives
 // hitting.glsl:17-38 — the root only.  fd: the roots as div_nr with ra =
 // rcp_nr(a), unless a lane's a = dot(dir, dir) is below 2^-60.
-// The ray's offset from the sphere's centre at `time`, o - (A + B time), with the x and y
-// operations as packed pairs (the same roundings).
-__device__ __forceinline__ v3 sphere_oc(float4 A, float4 B, float time, v3 o) {
-    const f2v cxy = f2v{A.x, A.y} + f2v{B.x, B.y} * time;
-    const f2v oxy = f2v{o.x, o.y} - cxy;
-    return mk3(oxy.x, oxy.y, o.z - (A.z + B.z * time));
-}
 __device__ __forceinline__ bool sphere_t_ab(float4 A, float4 B, float time, v3 o, v3 d, float a, float tmin,
                                             float tmax, float& t, bool fd = false, float ra = 0.0f) {
-    v3 oc = sphere_oc(A, B, time, o);
+    v3 center = add3(f3(A), scale3(f3(B), time));
+    v3 oc = sub3(o, center);
     float half_b = g_dot(oc, d);
     float c = g_dot(oc, oc) - B.w * B.w;
     float disc = half_b * half_b - a * c;
     if (disc < 0.0f) return false;
     float sq = sqrtf(disc);
     fd = fd && __ballot(!(a >= 0x1p-60f)) == 0;
-    if (fd) {   // both roots as one packed pair (the second is read only when the first fails)
-        const f2v r = div_nr2(f2v{-half_b - sq, -half_b + sq}, f2v{a, a}, f2v{ra, ra});
-        float root = r.x;
-        if (!(tmin < root && root < tmax)) {
-            root = r.y;
-            if (!(tmin < root && root < tmax)) return false;
-        }
-        t = root;
-        return true;
-    }
-    float root = (-half_b - sq) / a;
+    float root = fd ? div_nr(-half_b - sq, a, ra) : (-half_b - sq) / a;
     if (!(tmin < root && root < tmax)) {
-        root = (-half_b + sq) / a;
+        root = fd ? div_nr(-half_b + sq, a, ra) : (-half_b + sq) / a;
         if (!(tmin < root && root < tmax)) return false;
     }
     t = root;
@@ -215,22 +186,17 @@ __device__ __forceinline__ bool sphere_t_ab(float4 A, float4 B, float time, v3 o
 // (false when the discriminant is negative); the division form as sphere_t_ab chooses it.
 __device__ __forceinline__ bool sphere_roots(float4 A, float4 B, float time, v3 o, v3 d, float a, float& lo, float& hi,
                                              bool fd) {
-    v3 oc = sphere_oc(A, B, time, o);
+    v3 center = add3(f3(A), scale3(f3(B), time));
+    v3 oc = sub3(o, center);
     float half_b = g_dot(oc, d);
     float c = g_dot(oc, oc) - B.w * B.w;
     float disc = half_b * half_b - a * c;
     if (disc < 0.0f) return false;
     float sq = sqrtf(disc);
     fd = fd && __ballot(!(a >= 0x1p-60f)) == 0;
-    if (fd) {
-        const float ra = rcp_nr(a);
-        const f2v r = div_nr2(f2v{-half_b - sq, -half_b + sq}, f2v{a, a}, f2v{ra, ra});
-        lo = r.x;
-        hi = r.y;
-    } else {
-        lo = (-half_b - sq) / a;
-        hi = (-half_b + sq) / a;
-    }
+    const float ra = fd ? rcp_nr(a) : 0.0f;
+    lo = fd ? div_nr(-half_b - sq, a, ra) : (-half_b - sq) / a;
+    hi = fd ? div_nr(-half_b + sq, a, ra) : (-half_b + sq) / a;
     return true;
 }
 __device__ __forceinline__ bool sphere_t(const float4* __restrict__ sp, float time, v3 o, v3 d, float a, float tmin,
@@ -252,16 +218,13 @@ __device__ __forceinline__ bool face_interior(float4 A, float4 B, v3 o, v3 d, fl
     const int cs = __float_as_int(B.w);
     float oa = (cs == 2) ? o.y : o.x, da = (cs == 2) ? d.y : d.x;
     float ob = (cs == 0) ? o.y : o.z, db = (cs == 0) ? d.y : d.z;
-    // (pa, pb) = (oa + da t - A.x, ob + db t - A.y), (na, nb) = (pa B.y - pb B.x, pb A.z - pa A.w):
-    // the same operations as packed pairs
-    const f2v pp = (f2v{oa, ob} + f2v{da, db} * t) - f2v{A.x, A.y};
-    const f2v nn = pp * f2v{B.y, A.z} - f2v{pp.y, pp.x} * f2v{B.x, A.w};
-    const float na = nn.x, nb = nn.y;
+    float pa = (oa + da * t) - A.x;
+    float pb = (ob + db * t) - A.y;
+    const float na = pa * B.y - pb * B.x, nb = pb * A.z - pa * A.w;
     if (fd && __ballot(!(fabsf(na) >= 0x1p-100f && fabsf(nb) >= 0x1p-100f)) == 0) {
         const float r = rcp_nr(B.z);
-        const f2v ab = div_nr2(nn, f2v{B.z, B.z}, f2v{r, r});
-        alpha = ab.x;
-        beta = ab.y;
+        alpha = div_nr(na, B.z, r);
+        beta = div_nr(nb, B.z, r);
     } else {
         alpha = na / B.z;
         beta = nb / B.z;
@@ -416,7 +379,8 @@ __device__ __noinline__ bool boundary_t(const KP& P, int idx, int type, v3 o, v3
 __device__ __forceinline__ bool sphere_bounds(float4 A, float4 B, v3 o, v3 d, float a, float time, float& t1,
                                               float& t2, bool fd = false) {
     {
-        v3 oc = sphere_oc(A, B, time, o);
+        v3 center = add3(f3(A), scale3(f3(B), time));
+        v3 oc = sub3(o, center);
         float half_b = g_dot(oc, d);
         float c = g_dot(oc, oc) - B.w * B.w;
         float disc = half_b * half_b - a * c;
@@ -426,15 +390,8 @@ __device__ __forceinline__ bool sphere_bounds(float4 A, float4 B, v3 o, v3 d, fl
         float sq = sqrtf(disc);
         fd = fd && __ballot(!(a >= 0x1p-60f)) == 0;
         const float ra = fd ? rcp_nr(a) : 0.0f;
-        float r_lo, r_hi;
-        if (fd) {
-            const f2v r = div_nr2(f2v{-half_b - sq, -half_b + sq}, f2v{a, a}, f2v{ra, ra});
-            r_lo = r.x;
-            r_hi = r.y;
-        } else {
-            r_lo = (-half_b - sq) / a;
-            r_hi = (-half_b + sq) / a;
-        }
+        float r_lo = fd ? div_nr(-half_b - sq, a, ra) : (-half_b - sq) / a;
+        float r_hi = fd ? div_nr(-half_b + sq, a, ra) : (-half_b + sq) / a;
         const bool lo_in = -RT_INFINITY < r_lo && r_lo < RT_INFINITY;
         const bool hi_in = -RT_INFINITY < r_hi && r_hi < RT_INFINITY;
         t1 = lo_in ? r_lo : r_hi;
@@ -573,6 +530,7 @@ __device__ __forceinline__ bool aabb_fast(float4 n0, float4 n1, v3 o, v3 inv, fl
 
 // aabb_fast with the six slab subtractions and products as packed pairs
 // (v_pk_add_f32 / v_pk_mul_f32: the same IEEE roundings, half the issue).
+typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bool aabb_pk(float4 n0, float4 n1, v3 o, v3 inv, float tmin, float tmax) {
     const f2v tx = (f2v{n0.x, n0.y} - f2v{o.x, o.x}) * f2v{inv.x, inv.x};
     const f2v ty = (f2v{n0.z, n0.w} - f2v{o.y, o.y}) * f2v{inv.y, inv.y};
