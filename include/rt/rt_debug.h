@@ -39,6 +39,12 @@ int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_ca
  * pre-test bounds: xmin, xmax, ymin, ymax, zmin, zmax); *n_nodes = tree + pre-test nodes. */
 int rt_debug_link_nodes_vbox(const void* bvh, size_t nbytes, const float* vbox, int n_box, void* out,
                              size_t out_cap, int* n_f4, int* n_nodes);
+/* The link-format nodes of `bvh` with the node collapse of option collapse (rt_capi.hip
+ * plan_collapse) planned for camera `cam` (rt_camera_ubo, 28 floats) and a width x height image;
+ * drop (may be NULL) gets one byte per threaded node (1 = left out), *n_dropped their count.
+ * Host-side, no device needed (tests/test_link_nodes.py replays the walk). */
+int rt_debug_collapse_links(const void* bvh, size_t nbytes, const float cam[28], int width, int height, void* out,
+                            size_t out_cap, int* n_f4, unsigned char* drop, size_t drop_cap, int* n_dropped);
 
 /* Host-only: the packed Perlin table rt_upload_texture keeps beside an R32F 6 x 256 texture
  * whose perm columns (3..5) hold whole numbers 0..255: 256 float4 (ranvec x, y, z; the three
@@ -127,6 +133,10 @@ enum {
     RT_OPTION_ZERO_DIR_END = 24,        /* a path whose next direction is vec3(0) (the no-
                                            light branch) ends in its shading pass with the
                                            miss colour its next bounce would give (1)       */
+    RT_OPTION_COLLAPSE = 25,            /* the link walk leaves out the inner nodes whose
+                                           tests a grid of camera rays says cost more than
+                                           they save (boxes nest: the same leaves, order
+                                           and ray_t; rt_capi.hip plan_collapse) (1)       */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };
@@ -147,6 +157,7 @@ int rt_debug_get_option(struct rt_ctx* ctx, int option, int* value);
  *   out[12] leaf record prefetch  out[13] shading tables in LDS (bits)  out[14] walk threshold
  *   out[15] the BVH the walk ran on: RT_BVH_REFERENCE (0) or RT_BVH_SAH (1, rt_set_bvh_mode)
  *   out[16] box pre-test nodes in the walk (option box_vnodes; 0 = none)
+ *   out[17] inner nodes the walk leaves out (option collapse; 0 = none)
  * n <= 20 ints are written; returns RT_ERR_STATE before the first render. */
 int rt_debug_last_launch(struct rt_ctx* ctx, int* out, int n);
 

@@ -14,6 +14,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -152,6 +154,11 @@ struct rt_ctx {
     std::vector<float4> boxc_host;  // the compact box records (host copy of Device::dboxc)
     bool box_vnodes = true;         // option box_vnodes
     bool zero_dir_end = true;       // option zero_dir_end (rt_kernel.hip render_stream)
+    bool collapse = true;           // option collapse: the walk leaves out inner nodes (plan_collapse)
+    bool walk_c = false;            // walk_links were built with a collapse plan ...
+    rt_camera_ubo walk_cam{};       // ... for this camera and image size
+    int walk_w = 0, walk_h = 0;
+    int n_dropped = 0;              // inner nodes the walk leaves out
     FastTables fast;
     std::vector<float4> links;   // build_links(dnodes), empty when unavailable
     int fast_gen = 0;
@@ -390,12 +397,19 @@ bool boxes_nest(const std::vector<rt_dnode>& dn) {
 // lowest addresses, the part a two-level launch stages in LDS.  Empty when there is
 // no BVH or it has more nodes than 16-bit indices address.
 std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vector<float>* vbox = nullptr,
-                                int* n_nodes_out = nullptr) {
+                                int* n_nodes_out = nullptr, const std::vector<uint8_t>* drop = nullptr) {
     std::vector<float4> out;
     const size_t n = dn.size();
     if (n_nodes_out) *n_nodes_out = 0;
     if (n == 0 || n > RT_LINK_MAX_NODES) return out;
     auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
+    // Node collapse (plan_collapse): a link that leads to a left-out inner node leads to its first
+    // child (threaded k + 1) instead, repeatedly; the left-out nodes keep their place, unreachable.
+    const bool dropping = drop && drop->size() == n && !(*drop)[0];
+    auto kept = [&](uint32_t k) {
+        while (dropping && k < n && (*drop)[k] && !is_leaf(k)) k++;
+        return k;
+    };
     std::vector<uint32_t> pos(n, 0xFFFFFFFFu), order;
     order.reserve(n);
     order.push_back(0);
@@ -431,7 +445,7 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
         nv += t1 ? 2 : 1;
     }
     const size_t N = n + nv;
-    if (N > RT_LINK_MAX_NODES) return build_links(dn, nullptr, n_nodes_out);
+    if (N > RT_LINK_MAX_NODES) return build_links(dn, nullptr, n_nodes_out, drop);
     size_t nl = 0;
     for (size_t k = 0; k < n; k++)
         if (is_leaf(k)) nl += vfirst[k] == 0xFFFFFFFFu ? 1 : (((dn[k].meta >> 20) & 0xFu) ? 2 : 1);
@@ -450,7 +464,7 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
     for (size_t k = 0; k < n; k++) {
         const rt_dnode& d = dn[k];
         const uint32_t skip = d.meta & 0xFFFFu;
-        const uint32_t skip_at = skip == RT_NODE_END ? RT_LINK_END : 32u * pos[skip];
+        const uint32_t skip_at = skip == RT_NODE_END ? RT_LINK_END : 32u * pos[kept(skip)];
         const uint32_t next_end = skip == RT_NODE_END ? RT_LINK_NEXT_END : skip_at;
         uint32_t hit;
         if (is_leaf(k) && vfirst[k] != 0xFFFFFFFFu) {
@@ -469,12 +483,99 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
             hit = RT_LINK_LEAF | li;
             leaves[li++] = make_uint2(((d.meta >> 16) & 0xFFu) | next_end << 8, d.prims);
         } else {
-            hit = 32u * pos[k + 1];
+            hit = 32u * pos[kept((uint32_t)k + 1)];
         }
         put(pos[k], d.xmin, d.xmax, d.ymin, d.ymax, d.zmin, d.zmax, hit, skip_at);
     }
     if (n_nodes_out) *n_nodes_out = (int)N;
     return out;
+}
+
+// Node collapse (option collapse): which inner nodes the link walk leaves out.  When every node's
+// box holds its children's (boxes_nest) and no box is flat, a walk that skips an inner node's test
+// and tests its children where it stood tests the same leaves in the same order under the same
+// ray_t: where the reference's test of the node misses, its children's tests miss too -- per axis
+// the slab values are monotone in the plane coordinates (rounding is monotone; with a component
+// of 1/dir infinite the fast form passes an axis only for o strictly inside the slab, the exact
+// form (rt_kernel_common.h slab) only for o inside or on it, both monotone under nesting) and the
+// interval test is monotone in ray_t.max, which only shrinks between a node and its later
+// children -- and so on down to the leaf nodes, which are always kept.  Only the number of node
+// tests changes: leaving node N out saves its V(N) tests and costs each child V(N) - H(N) more,
+// where H(N), the tests of N that hit, does not depend on the other choices and V(N) = H of N's
+// nearest kept ancestor.  H is counted over a 128 x 72 grid of the camera's rays (pixel centres,
+// ray_t [0.001, inf), boxes only: the host traces no prims) and the least-tests choice for those
+// counts taken by a dynamic programme over the tree; the root stays (the walk starts there).
+// tools/node_collapse_study.py: on scene 8 this grid's choice cuts the node tests of the
+// reference's own walks by 11.5% beyond the spine (the best choice for the walks themselves: 16%).
+std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height) {
+    const size_t n = dn.size();
+    std::vector<uint8_t> drop(n, 0);
+    if (n < 3 || n > RT_LINK_MAX_NODES || width <= 0 || height <= 0 || !boxes_nest(dn)) return drop;
+    for (const rt_dnode& d : dn)
+        if (!(d.xmin < d.xmax && d.ymin < d.ymax && d.zmin < d.zmax)) return drop;
+    auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
+    const int gx = 128, gy = 72;
+    std::vector<int64_t> H(n, 0);
+    for (int j = 0; j < gy; j++) {
+        for (int i = 0; i < gx; i++) {
+            const float px = ((float)i + 0.5f) * (float)width / (float)gx;
+            const float py = ((float)j + 0.5f) * (float)height / (float)gy;
+            float o[3], inv[3];
+            for (int k = 0; k < 3; k++) {
+                o[k] = cam.camera_pos[k];
+                const float d = cam.up_left[k] + cam.pixel_delta_u[k] * px + cam.pixel_delta_v[k] * py - o[k];
+                inv[k] = 1.0f / d;
+            }
+            uint32_t k = 0;
+            while (k < n) {
+                const rt_dnode& b = dn[k];
+                const float lo3[3] = {b.xmin, b.ymin, b.zmin}, hi3[3] = {b.xmax, b.ymax, b.zmax};
+                float lo = 0.001f, hi = INFINITY;
+                for (int a = 0; a < 3; a++) {
+                    const float t0 = (lo3[a] - o[a]) * inv[a], t1 = (hi3[a] - o[a]) * inv[a];
+                    lo = std::fmax(lo, std::fmin(t0, t1));
+                    hi = std::fmin(hi, std::fmax(t0, t1));
+                }
+                const uint32_t skip = b.meta & 0xFFFFu;
+                if (!(hi <= lo)) {
+                    H[k]++;
+                    k = is_leaf(k) ? skip : k + 1;
+                } else {
+                    k = skip;
+                }
+                if (k == RT_NODE_END) break;
+            }
+        }
+    }
+    // cost(k, v): the fewest tests of k's subtree when k's place is reached v times
+    std::map<std::pair<uint32_t, int64_t>, std::pair<int64_t, bool>> memo;
+    std::function<std::pair<int64_t, bool>(uint32_t, int64_t)> cost = [&](uint32_t k, int64_t v) {
+        if (is_leaf(k)) return std::make_pair(v, false);
+        const auto key = std::make_pair(k, v);
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+        const uint32_t r = k + 1, l = dn[k + 1].meta & 0xFFFFu;
+        const int64_t keep = v + cost(r, H[k]).first + cost(l, H[k]).first;
+        std::pair<int64_t, bool> best(keep, false);
+        if (k != 0) {
+            const int64_t out = cost(r, v).first + cost(l, v).first;
+            if (out < keep) best = std::make_pair(out, true);
+        }
+        memo.emplace(key, best);
+        return best;
+    };
+    std::vector<std::pair<uint32_t, int64_t>> st{{0u, (int64_t)gx * gy}};
+    while (!st.empty()) {
+        const auto [k, v] = st.back();
+        st.pop_back();
+        if (is_leaf(k)) continue;
+        const bool out = cost(k, v).second;
+        drop[k] = out ? 1 : 0;
+        const uint32_t r = k + 1, l = dn[k + 1].meta & 0xFFFFu;
+        st.push_back({r, out ? v : H[k]});
+        st.push_back({l, out ? v : H[k]});
+    }
+    return drop;
 }
 
 // The default walk round threshold (option walk_frac 0): a round's node walk stops once this
@@ -1753,7 +1854,17 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         const bool all_cmp = c->compact_boxes && nb > 0 && c->n_boxc_ok == (int)nb;
         const bool use_v = c->box_vnodes && all_cmp && a.box_margin > 0.0f && (c->variant == 0 || c->variant == 39) &&
                            c->boxc_host.size() == nb * RT_BOXC_F4;
-        if (c->walk_stale || use_v != c->walk_v || (use_v && a.box_margin != c->walk_v_margin)) {
+        // node collapse (plan_collapse): planned for the camera, so rebuilt when it or the image size changes
+        const bool use_c = c->collapse && (c->variant == 0 || c->variant == 39) && c->have_cam;
+        const bool cam_moved = use_c && (std::memcmp(&c->walk_cam, &c->cam, sizeof(rt_camera_ubo)) != 0 ||
+                                         c->walk_w != c->width || c->walk_h != c->height);
+        if (c->walk_stale || use_v != c->walk_v || (use_v && a.box_margin != c->walk_v_margin) ||
+            use_c != c->walk_c || cam_moved) {
+            std::vector<uint8_t> drop;
+            if (use_c) drop = plan_collapse(c->walk_dn, c->cam, c->width, c->height);
+            c->n_dropped = 0;
+            for (uint8_t x : drop) c->n_dropped += x;
+            const std::vector<uint8_t>* dp = c->n_dropped ? &drop : nullptr;
             if (use_v) {
                 // the kernel's pre-test bounds (leaf_prims_t): compact record c0 = (mn.x, mn.y, mn.z,
                 // mx.x), c1 = (mx.y, mx.z, ..), each grown by the margin with the same float operations
@@ -1765,12 +1876,20 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                     std::memcpy(&vb[6 * b], g, sizeof(g));
                 }
                 int nn = 0;
-                c->walk_links = build_links(c->walk_dn, &vb, &nn);
+                c->walk_links = build_links(c->walk_dn, &vb, &nn, dp);
+                c->n_walk_nodes = nn;
+            } else if (dp) {
+                int nn = 0;
+                c->walk_links = build_links(c->walk_dn, nullptr, &nn, dp);
                 c->n_walk_nodes = nn;
             } else {
                 c->walk_links = c->links;
                 c->n_walk_nodes = c->n_link_nodes;
             }
+            c->walk_c = use_c;
+            c->walk_cam = c->cam;
+            c->walk_w = c->width;
+            c->walk_h = c->height;
             c->walk_v = use_v;
             c->walk_v_margin = use_v ? a.box_margin : -1.0f;
             c->walk_stale = false;
@@ -2077,6 +2196,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             if (&d == &c->devs[0]) {
                 c->last_launch[RT_LI_BVH_MODE] = c->bvh_mode;
                 c->last_launch[RT_LI_VNODES] = a.box_vnodes ? c->n_walk_nodes - c->n_link_nodes : 0;
+                c->last_launch[RT_LI_COLLAPSED] = c->walk_c ? c->n_dropped : 0;
             }
         }
         HIPCHK(c, hipEventRecord(d.ev_stop, d.stream));
@@ -2298,6 +2418,33 @@ int rt_debug_link_nodes_vbox(const void* bvh, size_t nbytes, const float* vbox, 
     return RT_OK;
 }
 
+int rt_debug_collapse_links(const void* bvh, size_t nbytes, const float cam[28], int width, int height, void* out,
+                            size_t out_cap, int* n_f4, uint8_t* drop, size_t drop_cap, int* n_dropped) {
+    if (!bvh || !cam || !n_f4 || !n_dropped || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
+    std::vector<rt_dnode> dn;
+    rt_ctx tmp;
+    int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
+    if (r) return r;
+    rt_camera_ubo cu;
+    std::memcpy(&cu, cam, sizeof(cu));
+    const std::vector<uint8_t> d = plan_collapse(dn, cu, width, height);
+    int nd = 0;
+    for (uint8_t x : d) nd += x;
+    *n_dropped = nd;
+    int nn = 0;
+    const std::vector<float4> L = build_links(dn, nullptr, &nn, &d);
+    *n_f4 = (int)L.size();
+    if (out) {
+        if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
+        std::memcpy(out, L.data(), L.size() * sizeof(float4));
+    }
+    if (drop) {
+        if (drop_cap < d.size()) return RT_ERR_INVALID_ARG;
+        std::memcpy(drop, d.data(), d.size());
+    }
+    return RT_OK;
+}
+
 int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_cap, int* n_f4) {
     if (!bvh || !n_f4 || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
     std::vector<rt_dnode> dn;
@@ -2440,6 +2587,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SHADE_LDS: c->shade_lds = v != 0; break;
         case RT_OPTION_BOX_VNODES: c->box_vnodes = v != 0; break;
         case RT_OPTION_ZERO_DIR_END: c->zero_dir_end = v != 0; break;
+        case RT_OPTION_COLLAPSE: c->collapse = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2479,6 +2627,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_SHADE_LDS: *v = c->shade_lds; break;
         case RT_OPTION_BOX_VNODES: *v = c->box_vnodes; break;
         case RT_OPTION_ZERO_DIR_END: *v = c->zero_dir_end; break;
+        case RT_OPTION_COLLAPSE: *v = c->collapse; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

@@ -31,7 +31,7 @@ pytestmark = pytest.mark.gpu
 
 CASES = adversarial.cases()
 OFF = [{}, {"box_pretest": 0}, {"fastdiv": 0}, {"compact_boxes": 0}, {"spine": 0}, {"shade_lds": 0},
-       {"box_vnodes": 0}, {"zero_dir_end": 0}]
+       {"box_vnodes": 0}, {"zero_dir_end": 0}, {"collapse": 0}]
 
 
 def oracle(case):

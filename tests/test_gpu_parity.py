@@ -210,3 +210,30 @@ def test_box_pretest_nodes_match_oracle(gpu, opts, expect):
                 if is_leaf(nd) and (int(nd["meta"]) >> 16) & 0xF == 4 and (int(nd["meta"]) >> 20) & 0xF in (0, 4))
         assert info["box_vnodes"] == n == 390, (info, n)
     assert bit_equal(out, ref), mismatch_report(out, ref)
+
+
+def test_collapsed_walk_matches_oracle_and_follows_the_camera(gpu):
+    """Round 5: the link walk leaves out the inner nodes a grid of camera rays says cost more tests
+    than they save (option collapse, on by default; rt_capi.hip plan_collapse).  Bit for bit against
+    the oracle; the plan is the host's for this camera and image size, and a moved camera re-plans
+    it (the launch reports the count the context-free planner gives for the new camera)."""
+    from test_link_nodes import collapse_links
+    s = rtamd.Scene(8, 48, 27, seed=1)
+    ctx = rtamd.RenderContext(devices=(0,))
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=4)
+    cams = [s.camera.copy(), s.camera.copy()]
+    cams[1][4:7] += np.float32([40.0, 25.0, -30.0])   # the same view, translated
+    cams[1][8:11] += np.float32([40.0, 25.0, -30.0])
+    for cam in cams:
+        s.override_camera(cam)
+        ctx.set_camera(s.camera)
+        ctx.resize(48, 27)
+        ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
+        out = ctx.read_image()
+        info = ctx.last_launch()
+        _, _, nd = collapse_links(s, 48, 27)
+        assert info["collapsed"] == nd > 0, (info, nd)
+        ref = oracle_image(s, 4, max_depth=5)
+        assert bit_equal(out, ref), mismatch_report(out, ref)
+    ctx.close()

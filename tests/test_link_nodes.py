@@ -252,3 +252,77 @@ def test_box_pretest_nodes_replay_the_walk(sid):
                     if slot_hits[first[k] + j]:
                         want.append((4 | PRETESTED, b))
             assert walk_links_n(ln, n_all, slot_hits) == want
+
+
+# ---- node collapse (option collapse, round 5) ------------------------------------------------------
+def collapse_links(scene, width=1920, height=1080, cam=None):
+    L = rtamd.amd()
+    b = scene.buffers[1]
+    bvh = ctypes.create_string_buffer(b, len(b))
+    cam = np.ascontiguousarray(scene.camera if cam is None else cam, np.float32)
+    n, nd = ctypes.c_int(), ctypes.c_int()
+    assert L.rt_debug_collapse_links(bvh, len(b), cam.ctypes.data, width, height, None, 0, ctypes.byref(n), None, 0,
+                                     ctypes.byref(nd)) == 0
+    out = np.zeros((max(n.value, 1), 4), np.float32)
+    m = len(b) // 32
+    drop = np.zeros(m, np.uint8)
+    assert L.rt_debug_collapse_links(bvh, len(b), cam.ctypes.data, width, height, out.ctypes.data, out.nbytes,
+                                     ctypes.byref(n), drop.ctypes.data, drop.nbytes, ctypes.byref(nd)) == 0
+    return out[:n.value], drop, nd.value
+
+
+def nested_hits(tn, rng, p):
+    """A random box-hit pattern in which a node hits only where its parent does (boxes nest, and the
+    slab test is monotone in the box: rt_capi.hip plan_collapse)."""
+    hits = np.zeros(len(tn), bool)
+    hits[0] = rng.random() < max(p, 0.5)
+    for k, nd in enumerate(tn):
+        if is_leaf(nd):
+            continue
+        for c in (k + 1, int(tn[k + 1]["meta"]) & 0xFFFF):
+            hits[c] = hits[k] and rng.random() < p
+    return hits
+
+
+@pytest.mark.parametrize("sid", [8, 0, 6, 7, 4])
+def test_collapsed_walk_tests_the_same_leaves(sid):
+    """Leaving out inner nodes (option collapse): under every nested pattern of box hits the walk
+    over the collapsed links tests the threaded walk's leaves in the same order, with fewer or more
+    node tests.  The links keep the tree's layout (the left-out nodes keep their places,
+    unreachable); the root and the leaf nodes are never left out."""
+    scene = rtamd.Scene(sid, 1920, 1080, seed=1)
+    tn = threaded(scene)
+    n = len(tn)
+    ln, drop, nd = collapse_links(scene)
+    plain = links_of(scene.buffers[1])
+    order = check_layout(tn, plain)
+    assert len(ln) == len(plain) and nd == int(drop.sum())
+    assert np.array_equal(ln[:2 * n].reshape(n, 8)[:, :6].view(np.uint32), plain[:2 * n].reshape(n, 8)[:, :6].view(np.uint32))
+    assert drop[0] == 0 and not any(drop[k] for k in range(n) if is_leaf(tn[k]))
+    if sid == 8:
+        assert nd > 100   # the fog's chain and much of the sphere cluster's upper levels
+    pos = np.empty(n, np.int64)
+    pos[order] = np.arange(n)
+    rng = np.random.default_rng(200 + sid)
+    steps_full = steps_coll = 0
+    for p in (0.3, 0.6, 0.9, 1.0):
+        for _ in range(25):
+            hits = nested_hits(tn, rng, p)
+            seen, want = walk_threaded(tn, hits)
+            s2, got = walk_links(ln, n, hits, order)
+            assert got == want
+            assert not any(drop[k] for k in s2)   # a left-out node is never reached
+            steps_full += len(seen)
+            steps_coll += len(s2)
+    assert steps_coll != steps_full or nd == 0
+
+
+def test_collapse_keeps_a_tree_whose_boxes_do_not_nest():
+    """No collapse unless every child box lies inside its parent's (boxes_nest) and no box is flat."""
+    rec = np.frombuffer(heap_bvh(64), dtype=[("box", "<f4", 6), ("l", "<u4"), ("r", "<u4")]).copy()
+    rec[5]["box"] = [-2, 2, -1, 1, -1, 1]   # an inner node wider than its parent
+    scene = rtamd.Scene(9, 64, 36, seed=1)
+    scene.buffers = dict(scene.buffers)
+    scene.buffers[1] = rec.tobytes()
+    _, drop, nd = collapse_links(scene)
+    assert nd == 0 and not drop.any()
