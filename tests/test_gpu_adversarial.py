@@ -60,8 +60,10 @@ def test_adversarial_case_matches_oracle(gpu, case):
         if not opts:
             for k, v in case.expect.items():
                 assert info[k] == v, f"{case.name}: launch {k} = {info[k]}, expected {v} ({info})"
-            if case.name.startswith("spine"):
-                assert info["spine"] == 6, info   # root + 5 right children (tests/adversarial.py spine_box)
+        elif "collapse" in opts and case.name.startswith("spine"):
+            # the reference tree's chain (with collapse the chain's always-hit nodes are left out
+            # of the walk instead): root + 5 right children (tests/adversarial.py spine_box)
+            assert info["spine"] == 6, info
         elif "spine" in opts:
             assert info["spine"] == 0, info
 
@@ -74,7 +76,9 @@ def test_scenes_walks_skip_their_spine(gpu, sid, spine):
     sphere's box).  The same bits as with the entry off and as the oracle."""
     s = rtamd.Scene(sid, 64, 48, seed=1)
     ref = pyoracle.render(pyoracle.OracleScene(s, max_depth=5, spp=4), rtamd.frame_rand_factors(1, 0, 4))
-    for opts, want in (({}, spine), ({"spine": 0}, 0)):
+    # on the reference tree's links (with node collapse, the default, the chain's nodes are left
+    # out of the walk altogether)
+    for opts, want in (({"collapse": 0}, spine), ({"collapse": 0, "spine": 0}, 0)):
         ctx = rtamd.RenderContext(options=opts)
         ctx.upload_scene(s)
         ctx.set_params(max_depth=5, spp=4)
