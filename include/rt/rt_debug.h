@@ -39,12 +39,15 @@ int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_ca
  * pre-test bounds: xmin, xmax, ymin, ymax, zmin, zmax); *n_nodes = tree + pre-test nodes. */
 int rt_debug_link_nodes_vbox(const void* bvh, size_t nbytes, const float* vbox, int n_box, void* out,
                              size_t out_cap, int* n_f4, int* n_nodes);
-/* The link-format nodes of `bvh` with the node collapse of option collapse (rt_capi.hip
- * plan_collapse) planned for camera `cam` (rt_camera_ubo, 28 floats) and a width x height image;
- * drop (may be NULL) gets one byte per threaded node (1 = left out), *n_dropped their count.
- * Host-side, no device needed (tests/test_link_nodes.py replays the walk). */
-int rt_debug_collapse_links(const void* bvh, size_t nbytes, const float cam[28], int width, int height, void* out,
-                            size_t out_cap, int* n_f4, unsigned char* drop, size_t drop_cap, int* n_dropped);
+/* The link-format nodes of `bvh` as the walk of a context uses them: with rebuild != 0 the inner
+ * nodes rebuilt over the leaf sequence (option rebuild, rt_capi.hip rebuild_inner), then the node
+ * collapse of option collapse (plan_collapse) planned for camera `cam` (rt_camera_ubo, 28
+ * floats) and a width x height image; drop (may be NULL) gets one byte per threaded node of that
+ * tree (1 = left out), *n_dropped their count.  Host-side, no device needed
+ * (tests/test_link_nodes.py replays the walk). */
+int rt_debug_collapse_links(const void* bvh, size_t nbytes, const float cam[28], int width, int height, int rebuild,
+                            void* out, size_t out_cap, int* n_f4, unsigned char* drop, size_t drop_cap,
+                            int* n_dropped);
 
 /* Host-only: the packed Perlin table rt_upload_texture keeps beside an R32F 6 x 256 texture
  * whose perm columns (3..5) hold whole numbers 0..255: 256 float4 (ranvec x, y, z; the three
@@ -137,6 +140,10 @@ enum {
                                            tests a grid of camera rays says cost more than
                                            they save (boxes nest: the same leaves, order
                                            and ray_t; rt_capi.hip plan_collapse) (1)       */
+    RT_OPTION_REBUILD = 26,             /* the link walk's inner nodes rebuilt over the
+                                           reference's leaf sequence (surface-area splits,
+                                           joined boxes: the same leaves, order and ray_t;
+                                           rt_capi.hip rebuild_inner) (1)                   */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };
@@ -158,6 +165,7 @@ int rt_debug_get_option(struct rt_ctx* ctx, int option, int* value);
  *   out[15] the BVH the walk ran on: RT_BVH_REFERENCE (0) or RT_BVH_SAH (1, rt_set_bvh_mode)
  *   out[16] box pre-test nodes in the walk (option box_vnodes; 0 = none)
  *   out[17] inner nodes the walk leaves out (option collapse; 0 = none)
+ *   out[18] the walk's inner nodes rebuilt over the leaf sequence (option rebuild; 1/0)
  * n <= 20 ints are written; returns RT_ERR_STATE before the first render. */
 int rt_debug_last_launch(struct rt_ctx* ctx, int* out, int n);
 

@@ -155,10 +155,13 @@ struct rt_ctx {
     bool box_vnodes = true;         // option box_vnodes
     bool zero_dir_end = true;       // option zero_dir_end (rt_kernel.hip render_stream)
     bool collapse = true;           // option collapse: the walk leaves out inner nodes (plan_collapse)
+    bool rebuild = true;            // option rebuild: the walk's inner nodes rebuilt over its leaves (rebuild_inner)
+    bool walk_r = false;            // walk_links were built on the rebuilt inner nodes
     bool walk_c = false;            // walk_links were built with a collapse plan ...
     rt_camera_ubo walk_cam{};       // ... for this camera and image size
     int walk_w = 0, walk_h = 0;
     int n_dropped = 0;              // inner nodes the walk leaves out
+    int n_rebuilt = 0;              // nodes of the rebuilt tree (0: the tree as uploaded / built)
     FastTables fast;
     std::vector<float4> links;   // build_links(dnodes), empty when unavailable
     int fast_gen = 0;
@@ -491,6 +494,93 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
     return out;
 }
 
+// Small trees (up to RT_SMALL_TREE nodes: the Cornell boxes' 7) keep their nodes: there the camera's
+// rays are few of the walks (paths bounce inside the box) and their counts mislead -- scenes 6 / 7
+// measured +7.7 / +13.8% with the grid's choice, while scene 0 (511 nodes) -8.8%, scene 8 -5.6%
+// (profiles/r05_j_opts_s*.log).
+#define RT_SMALL_TREE 64
+
+// Inner-node rebuild (option rebuild): the walk's leaves tested, their order and each test's
+// ray_t do not depend on the inner nodes above them, as long as every inner box holds the leaf
+// boxes below it.  A leaf node whose box test hits (under the ray_t of its turn) has every
+// ancestor's test hit too -- an ancestor is tested earlier, under a ray_t.max at least as large,
+// and the slab test is monotone in the box and in ray_t.max (plan_collapse below) -- so it is
+// tested in any such tree; one whose test misses has its prims tested in none.  The leaves' own
+// boxes and their order (the reference's walk order, the threaded array's) decide everything.  So
+// the inner nodes are rebuilt over the reference's leaf sequence: each range of consecutive leaves
+// split where the surface-area cost of its two parts, area x leaves, is least, a node's box the
+// exact join (min / max) of its leaves' boxes.  The reference's builder splits at the median along
+// a random axis (BVHNode.java:13-56); over scene 8's leaf order this tree takes a camera ray
+// through 35% fewer node tests (tools/node_collapse_study.py).  Leaves and their records are
+// unchanged.  Empty when a leaf box is flat or inverted (plan_collapse's condition) or the
+// tree has fewer than 3 leaves.
+std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn) {
+    std::vector<rt_dnode> out;
+    const size_t n = dn.size();
+    if (n <= RT_SMALL_TREE || n > RT_LINK_MAX_NODES) return out;
+    std::vector<uint32_t> L;
+    for (size_t k = 0; k < n; k++) {
+        const rt_dnode& d = dn[k];
+        if ((d.meta & 0xF0000u) == 0) continue;
+        if (!(d.xmin < d.xmax && d.ymin < d.ymax && d.zmin < d.zmax)) return out;
+        L.push_back((uint32_t)k);
+    }
+    const size_t m = L.size();
+    if (m < 3 || 2 * m - 1 > RT_LINK_MAX_NODES) return out;
+    auto join = [](rt_dnode& a, const rt_dnode& b) {
+        a.xmin = std::min(a.xmin, b.xmin); a.xmax = std::max(a.xmax, b.xmax);
+        a.ymin = std::min(a.ymin, b.ymin); a.ymax = std::max(a.ymax, b.ymax);
+        a.zmin = std::min(a.zmin, b.zmin); a.zmax = std::max(a.zmax, b.zmax);
+    };
+    auto area = [](const rt_dnode& b) {
+        const double dx = (double)b.xmax - b.xmin, dy = (double)b.ymax - b.ymin, dz = (double)b.zmax - b.zmin;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    out.resize(2 * m - 1);
+    std::vector<rt_dnode> pre(m), suf(m);
+    // pre-order emission: (range, slot); a node's first child follows it, its skip is the slot
+    // after its subtree (2 x leaves - 1 slots), RT_NODE_END past the last
+    struct Item { uint32_t i, j, at; };
+    std::vector<Item> st{{0u, (uint32_t)m, 0u}};
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        const uint32_t cnt = it.j - it.i, end = it.at + 2 * cnt - 1;
+        const uint32_t skip = end >= 2 * m - 1 ? RT_NODE_END : end;
+        if (cnt == 1) {
+            rt_dnode d = dn[L[it.i]];
+            d.meta = (d.meta & ~0xFFFFu) | skip;
+            out[it.at] = d;
+            continue;
+        }
+        for (uint32_t t = 0; t < cnt; t++) {
+            pre[t] = dn[L[it.i + t]];
+            if (t) join(pre[t], pre[t - 1]);
+        }
+        for (uint32_t t = cnt; t-- > 0;) {
+            suf[t] = dn[L[it.i + t]];
+            if (t + 1 < cnt) join(suf[t], suf[t + 1]);
+        }
+        uint32_t best = 1;
+        double best_c = INFINITY;
+        for (uint32_t s = 1; s < cnt; s++) {
+            const double cst = area(pre[s - 1]) * s + area(suf[s]) * (cnt - s);
+            if (cst < best_c) {
+                best_c = cst;
+                best = s;
+            }
+        }
+        rt_dnode d = pre[cnt - 1];
+        d.meta = skip;   // inner: no prim types
+        d.prims = 0;
+        out[it.at] = d;
+        const uint32_t first_at = it.at + 1, second_at = it.at + 1 + (2 * best - 1);
+        st.push_back({it.i + best, it.j, second_at});
+        st.push_back({it.i, it.i + best, first_at});
+    }
+    return out;
+}
+
 // Node collapse (option collapse): which inner nodes the link walk leaves out.  When every node's
 // box holds its children's (boxes_nest) and no box is flat, a walk that skips an inner node's test
 // and tests its children where it stood tests the same leaves in the same order under the same
@@ -510,7 +600,7 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
 std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height) {
     const size_t n = dn.size();
     std::vector<uint8_t> drop(n, 0);
-    if (n < 3 || n > RT_LINK_MAX_NODES || width <= 0 || height <= 0 || !boxes_nest(dn)) return drop;
+    if (n <= RT_SMALL_TREE || n > RT_LINK_MAX_NODES || width <= 0 || height <= 0 || !boxes_nest(dn)) return drop;
     for (const rt_dnode& d : dn)
         if (!(d.xmin < d.xmax && d.ymin < d.ymax && d.zmin < d.zmax)) return drop;
     auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
@@ -585,7 +675,7 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
 // (-1.3%), scene 8's 1793 nodes 48..52 (44: +0.4%); a two-level launch takes 32 (LDS plan below).
 // Rounds only regroup which lanes walk and
 // test leaves together: every lane's node and prim sequence is unchanged (bit-identical).
-int walk_frac_for(int n_nodes) { return n_nodes <= 64 ? 8 : n_nodes <= 1024 ? 32 : 48; }
+int walk_frac_for(int n_nodes) { return n_nodes <= RT_SMALL_TREE ? 8 : n_nodes <= 1024 ? 32 : 48; }
 
 // The spine of the link-format walk (rt_kernel.hip spine_entry): every walk starts at the
 // root and, while it hits, goes on to the right child (compute.glsl:259-260), so its first
@@ -1858,10 +1948,14 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         const bool use_c = c->collapse && (c->variant == 0 || c->variant == 39) && c->have_cam;
         const bool cam_moved = use_c && (std::memcmp(&c->walk_cam, &c->cam, sizeof(rt_camera_ubo)) != 0 ||
                                          c->walk_w != c->width || c->walk_h != c->height);
+        const bool use_r = c->rebuild && (c->variant == 0 || c->variant == 39);
         if (c->walk_stale || use_v != c->walk_v || (use_v && a.box_margin != c->walk_v_margin) ||
-            use_c != c->walk_c || cam_moved) {
+            use_c != c->walk_c || cam_moved || use_r != c->walk_r) {
+            std::vector<rt_dnode> rb;
+            if (use_r) rb = rebuild_inner(c->walk_dn);
+            const std::vector<rt_dnode>& wdn = rb.empty() ? c->walk_dn : rb;
             std::vector<uint8_t> drop;
-            if (use_c) drop = plan_collapse(c->walk_dn, c->cam, c->width, c->height);
+            if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height);
             c->n_dropped = 0;
             for (uint8_t x : drop) c->n_dropped += x;
             const std::vector<uint8_t>* dp = c->n_dropped ? &drop : nullptr;
@@ -1876,17 +1970,19 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                     std::memcpy(&vb[6 * b], g, sizeof(g));
                 }
                 int nn = 0;
-                c->walk_links = build_links(c->walk_dn, &vb, &nn, dp);
+                c->walk_links = build_links(wdn, &vb, &nn, dp);
                 c->n_walk_nodes = nn;
-            } else if (dp) {
+            } else if (dp || !rb.empty()) {
                 int nn = 0;
-                c->walk_links = build_links(c->walk_dn, nullptr, &nn, dp);
+                c->walk_links = build_links(wdn, nullptr, &nn, dp);
                 c->n_walk_nodes = nn;
             } else {
                 c->walk_links = c->links;
                 c->n_walk_nodes = c->n_link_nodes;
             }
             c->walk_c = use_c;
+            c->walk_r = use_r;
+            c->n_rebuilt = rb.empty() ? 0 : (int)rb.size();
             c->walk_cam = c->cam;
             c->walk_w = c->width;
             c->walk_h = c->height;
@@ -2197,6 +2293,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                 c->last_launch[RT_LI_BVH_MODE] = c->bvh_mode;
                 c->last_launch[RT_LI_VNODES] = a.box_vnodes ? c->n_walk_nodes - c->n_link_nodes : 0;
                 c->last_launch[RT_LI_COLLAPSED] = c->walk_c ? c->n_dropped : 0;
+                c->last_launch[RT_LI_REBUILT] = c->n_rebuilt > 0 ? 1 : 0;
             }
         }
         HIPCHK(c, hipEventRecord(d.ev_stop, d.stream));
@@ -2418,13 +2515,17 @@ int rt_debug_link_nodes_vbox(const void* bvh, size_t nbytes, const float* vbox, 
     return RT_OK;
 }
 
-int rt_debug_collapse_links(const void* bvh, size_t nbytes, const float cam[28], int width, int height, void* out,
-                            size_t out_cap, int* n_f4, uint8_t* drop, size_t drop_cap, int* n_dropped) {
+int rt_debug_collapse_links(const void* bvh, size_t nbytes, const float cam[28], int width, int height, int rebuild,
+                            void* out, size_t out_cap, int* n_f4, uint8_t* drop, size_t drop_cap, int* n_dropped) {
     if (!bvh || !cam || !n_f4 || !n_dropped || nbytes % sizeof(rt_bvh_node)) return RT_ERR_INVALID_ARG;
     std::vector<rt_dnode> dn;
     rt_ctx tmp;
     int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
     if (r) return r;
+    if (rebuild) {
+        std::vector<rt_dnode> rb = rebuild_inner(dn);
+        if (!rb.empty()) dn.swap(rb);
+    }
     rt_camera_ubo cu;
     std::memcpy(&cu, cam, sizeof(cu));
     const std::vector<uint8_t> d = plan_collapse(dn, cu, width, height);
@@ -2588,6 +2689,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_BOX_VNODES: c->box_vnodes = v != 0; break;
         case RT_OPTION_ZERO_DIR_END: c->zero_dir_end = v != 0; break;
         case RT_OPTION_COLLAPSE: c->collapse = v != 0; break;
+        case RT_OPTION_REBUILD: c->rebuild = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
@@ -2628,6 +2730,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_BOX_VNODES: *v = c->box_vnodes; break;
         case RT_OPTION_ZERO_DIR_END: *v = c->zero_dir_end; break;
         case RT_OPTION_COLLAPSE: *v = c->collapse; break;
+        case RT_OPTION_REBUILD: *v = c->rebuild; break;
         case RT_OPTION_CHUNK_TARGET: *v = c->chunk_target; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: *v = c->staged_chunk_target; break;
         case RT_OPTION_STAGE_TILES: *v = c->stage_tiles; break;

@@ -197,7 +197,7 @@ struct rt_kernel_args {
 
 // What rt_launch_render launched (rt_debug_last_launch)
 enum { RT_LI_SHAPE = 0, RT_LI_BLOCK, RT_LI_FASTDIV, RT_LI_PRETEST, RT_LI_LDS, RT_LI_LDS_NODES, RT_LI_COMPACT,
-       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_LEAF_PF, RT_LI_SHADE_LDS, RT_LI_WALK_FRAC, RT_LI_BVH_MODE, RT_LI_VNODES, RT_LI_COLLAPSED, RT_LI_N = 20 };
+       RT_LI_STAGED, RT_LI_CHUNKS, RT_LI_SPINE, RT_LI_SPARSE, RT_LI_SPAIR, RT_LI_LEAF_PF, RT_LI_SHADE_LDS, RT_LI_WALK_FRAC, RT_LI_BVH_MODE, RT_LI_VNODES, RT_LI_COLLAPSED, RT_LI_REBUILT, RT_LI_N = 20 };
 
 #ifdef RT_AB_KNOBS
 // A/B library only (rt_kernel_variants.hip): the structures the release library does not ship

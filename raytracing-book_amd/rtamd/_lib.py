@@ -97,7 +97,7 @@ def _amd_protos(L):
     _proto(L, "rt_debug_fast_tables", i, vp, sz, vp, sz, vp, sz, i, vp, sz, c_int_p,
            ctypes.POINTER(ctypes.c_uint32), sz, c_int_p, c_int_p)
     _proto(L, "rt_debug_link_nodes", i, vp, sz, vp, sz, c_int_p)
-    _proto(L, "rt_debug_collapse_links", i, vp, sz, vp, i, i, vp, sz, c_int_p, vp, sz, c_int_p)
+    _proto(L, "rt_debug_collapse_links", i, vp, sz, vp, i, i, i, vp, sz, c_int_p, vp, sz, c_int_p)
     _proto(L, "rt_debug_link_nodes_vbox", i, vp, sz, c_float_p, i, vp, sz, c_int_p, c_int_p)
     _proto(L, "rt_debug_box_records", i, vp, sz, vp, sz, c_int_p)
     _proto(L, "rt_debug_perlin_pack", i, c_float_p, i, i, vp, sz)

@@ -255,19 +255,20 @@ def test_box_pretest_nodes_replay_the_walk(sid):
 
 
 # ---- node collapse (option collapse, round 5) ------------------------------------------------------
-def collapse_links(scene, width=1920, height=1080, cam=None):
+def collapse_links(scene, width=1920, height=1080, cam=None, rebuild=0):
     L = rtamd.amd()
     b = scene.buffers[1]
     bvh = ctypes.create_string_buffer(b, len(b))
     cam = np.ascontiguousarray(scene.camera if cam is None else cam, np.float32)
     n, nd = ctypes.c_int(), ctypes.c_int()
-    assert L.rt_debug_collapse_links(bvh, len(b), cam.ctypes.data, width, height, None, 0, ctypes.byref(n), None, 0,
-                                     ctypes.byref(nd)) == 0
+    assert L.rt_debug_collapse_links(bvh, len(b), cam.ctypes.data, width, height, rebuild, None, 0, ctypes.byref(n),
+                                     None, 0, ctypes.byref(nd)) == 0
     out = np.zeros((max(n.value, 1), 4), np.float32)
     m = len(b) // 32
     drop = np.zeros(m, np.uint8)
-    assert L.rt_debug_collapse_links(bvh, len(b), cam.ctypes.data, width, height, out.ctypes.data, out.nbytes,
-                                     ctypes.byref(n), drop.ctypes.data, drop.nbytes, ctypes.byref(nd)) == 0
+    assert L.rt_debug_collapse_links(bvh, len(b), cam.ctypes.data, width, height, rebuild, out.ctypes.data,
+                                     out.nbytes, ctypes.byref(n), drop.ctypes.data, drop.nbytes,
+                                     ctypes.byref(nd)) == 0
     return out[:n.value], drop, nd.value
 
 
@@ -326,3 +327,110 @@ def test_collapse_keeps_a_tree_whose_boxes_do_not_nest():
     scene.buffers[1] = rec.tobytes()
     _, drop, nd = collapse_links(scene)
     assert nd == 0 and not drop.any()
+
+
+# ---- inner-node rebuild (option rebuild, round 5) -------------------------------------------------
+def slab_hit(b, o, inv, tmin, tmax, exact):
+    """The kernel's node test on float32 values: the NaN-ignoring min / max form (aabb_pk), or, for
+    a ray with a -inf component of 1/dir, the reference's per-axis slab (rt_kernel_common.h slab)."""
+    t0 = (np.float32(b[0::2]) - o) * inv
+    t1 = (np.float32(b[1::2]) - o) * inv
+    if not exact:
+        lo = np.fmax(np.float32(tmin), np.fmax.reduce(np.fmin(t0, t1)))
+        hi = np.fmin(np.float32(tmax), np.fmin.reduce(np.fmax(t0, t1)))
+        return not (hi <= lo)
+    lo, hi = np.float32(tmin), np.float32(tmax)
+    for k in range(3):
+        ordr = t0[k] < t1[k]
+        a, c = (t0[k], t1[k]) if ordr else (t1[k], t0[k])
+        lo = a if a > lo else lo
+        hi = c if c < hi else hi
+    return not (hi <= lo)
+
+
+def shrink(prims, o, d, tmax, box):
+    """A leaf's tests as the walks see them: deterministic in (leaf, ray, ray_t.max) -- some leaves
+    'hit' at the distance to their box centre when it is closer than ray_t.max."""
+    if hash(int(prims)) % 3:
+        return tmax
+    c = np.float32([(box[0] + box[1]) / 2, (box[2] + box[3]) / 2, (box[4] + box[5]) / 2])
+    t = np.float32(np.dot(c - o, d) / max(np.dot(d, d), np.float32(1e-30)))
+    return t if 0.001 < t < tmax else tmax
+
+
+def walk_tree_rays(tn, o, d, inv, exact):
+    i, tmax, tested = 0, np.float32(np.inf), []
+    while i != END:
+        nd = tn[i]
+        skip = int(nd["meta"]) & 0xFFFF
+        if not slab_hit(nd["box"], o, inv, 0.001, tmax, exact):
+            i = skip
+        elif is_leaf(nd):
+            tested.append((int(nd["prims"]), float(tmax)))
+            tmax = shrink(nd["prims"], o, d, tmax, nd["box"])
+            i = skip
+        else:
+            i += 1
+    return tested
+
+
+def walk_links_rays(ln, n, o, d, inv, exact):
+    words = ln.view(np.uint32)
+    leaves = words[2 * n:].reshape(-1, 2)
+    nx, tmax, tested = 0, np.float32(np.inf), []
+    last_box = None
+    while True:
+        while nx < LEAF:
+            at = nx // 32
+            box = np.concatenate([ln[2 * at], ln[2 * at + 1][:2]])
+            h = slab_hit(box, o, inv, 0.001, tmax, exact)
+            if h:
+                last_box = box
+            nx = int(words[2 * at + 1, 2] if h else words[2 * at + 1, 3])
+        if nx == LEND:
+            break
+        lf = leaves[nx & 0x7FFFFFFF]
+        tested.append((int(lf[1]), float(tmax)))
+        tmax = shrink(lf[1], o, d, tmax, last_box)
+        nx = int(lf[0]) >> 8
+        if nx == NEXT_END:
+            break
+    return tested
+
+
+@pytest.mark.parametrize("sid", [8, 0, 6])
+def test_rebuilt_inner_nodes_test_the_same_leaves(sid):
+    """The inner nodes rebuilt over the reference's leaf sequence (option rebuild), then collapsed
+    (option collapse): for rays through the scene -- some with a zero direction component (1/dir
+    = +-inf), ray_t.max shrinking at some leaves -- the walk over the links tests the reference
+    tree's leaves in the same order under the same ray_t.max.  Nothing about the inner nodes
+    matters but that their boxes hold the leaves' (rt_capi.hip rebuild_inner)."""
+    scene = rtamd.Scene(sid, 1920, 1080, seed=1)
+    tn = threaded(scene)
+    n = len(tn)
+    ln, drop, nd = collapse_links(scene, rebuild=1)
+    leaves_tn = [(int(x["meta"]) >> 16 & 0xFF, int(x["prims"])) for x in tn if is_leaf(x)]
+    w = ln.view(np.uint32)
+    rec = [(int(a) & 0xFF, int(b)) for a, b in w[2 * n:].reshape(-1, 2)][:len(leaves_tn)]
+    assert rec == leaves_tn   # the same leaf records, in the same order
+    boxes = np.stack([x["box"] for x in tn])
+    lo, hi = boxes[0, 0::2], boxes[0, 1::2]
+    lo, hi = np.maximum(lo, -600), np.minimum(hi, 600)
+    rng = np.random.default_rng(300 + sid)
+    cam = scene.camera[4:7].astype(np.float32)
+    differ = 0
+    for r in range(300):
+        o = cam if r % 3 == 0 else (lo + (hi - lo) * rng.random(3)).astype(np.float32)
+        d = rng.normal(size=3).astype(np.float32)
+        if r % 7 == 0:
+            d[rng.integers(3)] = 0.0
+        if r % 11 == 0:
+            d[rng.integers(3)] = -0.0
+        with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+            inv = (np.float32(1.0) / d).astype(np.float32)
+            exact = bool(np.any(inv == -np.inf))
+            want = walk_tree_rays(tn, o, d, inv, exact)
+            got = walk_links_rays(ln, n, o, d, inv, exact)
+        assert got == want, (r, o, d)
+        differ += len(want) > 0
+    assert differ > 50
