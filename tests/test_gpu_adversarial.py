@@ -31,7 +31,7 @@ pytestmark = pytest.mark.gpu
 
 CASES = adversarial.cases()
 OFF = [{}, {"box_pretest": 0}, {"fastdiv": 0}, {"compact_boxes": 0}, {"spine": 0}, {"shade_lds": 0},
-       {"box_vnodes": 0}, {"zero_dir_end": 0}, {"collapse": 0}]
+       {"box_vnodes": 0}, {"zero_dir_end": 0}, {"rebuild": 0}, {"collapse": 0, "rebuild": 0}]
 
 
 def oracle(case):
@@ -76,9 +76,9 @@ def test_scenes_walks_skip_their_spine(gpu, sid, spine):
     sphere's box).  The same bits as with the entry off and as the oracle."""
     s = rtamd.Scene(sid, 64, 48, seed=1)
     ref = pyoracle.render(pyoracle.OracleScene(s, max_depth=5, spp=4), rtamd.frame_rand_factors(1, 0, 4))
-    # on the reference tree's links (with node collapse, the default, the chain's nodes are left
-    # out of the walk altogether)
-    for opts, want in (({"collapse": 0}, spine), ({"collapse": 0, "spine": 0}, 0)):
+    # on the reference tree's links (with the inner-node rebuild and collapse, the defaults, the
+    # chain is gone: the rebuilt tree splits the fog's leaf off at the root)
+    for opts, want in (({"collapse": 0, "rebuild": 0}, spine), ({"collapse": 0, "rebuild": 0, "spine": 0}, 0)):
         ctx = rtamd.RenderContext(options=opts)
         ctx.upload_scene(s)
         ctx.set_params(max_depth=5, spp=4)

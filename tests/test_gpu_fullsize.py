@@ -157,7 +157,7 @@ WALK_OPTIONS = [
     ("walk_frac", {"walk_frac": 16}), ("walk_frac", {"walk_frac": 48}), ("walk_frac", {"walk_frac": 64}),
     ("sphere_pairs", {"sphere_pairs": 0}), ("spine", {"spine": 0}), ("leaf_prefetch", {"leaf_prefetch": 0}),
     ("shade_lds", {"shade_lds": 0}), ("box_vnodes", {"box_vnodes": 0}), ("zero_dir_end", {"zero_dir_end": 0}),
-    ("collapse", {"collapse": 0}),
+    ("collapse", {"collapse": 0}), ("rebuild", {"rebuild": 0}), ("rebuild", {"rebuild": 0, "collapse": 0}),
     ("two_level", {"lds_node_cap": 16384}), ("two_level_leaf_global", {"lds_node_cap": 16384, "tl_leaf_lds": 0}),
 ]
 
