@@ -154,11 +154,10 @@ struct rt_ctx {
     std::vector<float4> boxc_host;  // the compact box records (host copy of Device::dboxc)
     bool box_vnodes = true;         // option box_vnodes
     bool zero_dir_end = true;       // option zero_dir_end (rt_kernel.hip render_stream)
-    int collapse = 1;               // option collapse: the walk leaves out inner nodes (plan_collapse mode)
+    bool collapse = true;           // option collapse: the walk leaves out inner nodes (plan_collapse)
     bool rebuild = true;            // option rebuild: the walk's inner nodes rebuilt over its leaves (rebuild_inner)
     bool walk_r = false;            // walk_links were built on the rebuilt inner nodes
     bool walk_c = false;            // walk_links were built with a collapse plan ...
-    int walk_cmode = 0;             // ... of this mode
     rt_camera_ubo walk_cam{};       // ... for this camera and image size
     int walk_w = 0, walk_h = 0;
     int n_dropped = 0;              // inner nodes the walk leaves out
@@ -598,73 +597,43 @@ std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn) {
 // counts taken by a dynamic programme over the tree; the root stays (the walk starts there).
 // tools/node_collapse_study.py: on scene 8 this grid's choice cuts the node tests of the
 // reference's own walks by 11.5% beyond the spine (the best choice for the walks themselves: 16%).
-std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height,
-                                   int mode = 1) {
+std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height) {
     const size_t n = dn.size();
     std::vector<uint8_t> drop(n, 0);
     if (n <= RT_SMALL_TREE || n > RT_LINK_MAX_NODES || width <= 0 || height <= 0 || !boxes_nest(dn)) return drop;
     for (const rt_dnode& d : dn)
         if (!(d.xmin < d.xmax && d.ymin < d.ymax && d.zmin < d.zmax)) return drop;
     auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
-    std::vector<int64_t> H(n, 0);
-    int64_t walks = 0;
-    // one box-only walk: counts the nodes it hits; returns the nearest entry distance into a leaf
-    // box that does not hold the origin (INFINITY: none)
-    auto walk = [&](const float o[3], const float d[3]) {
-        float inv[3];
-        for (int a = 0; a < 3; a++) inv[a] = 1.0f / d[a];
-        float near = INFINITY;
-        uint32_t k = 0;
-        walks++;
-        while (k < n) {
-            const rt_dnode& b = dn[k];
-            const float lo3[3] = {b.xmin, b.ymin, b.zmin}, hi3[3] = {b.xmax, b.ymax, b.zmax};
-            float lo = 0.001f, hi = INFINITY;
-            for (int a = 0; a < 3; a++) {
-                const float t0 = (lo3[a] - o[a]) * inv[a], t1 = (hi3[a] - o[a]) * inv[a];
-                lo = std::fmax(lo, std::fmin(t0, t1));
-                hi = std::fmin(hi, std::fmax(t0, t1));
-            }
-            const uint32_t skip = b.meta & 0xFFFFu;
-            if (!(hi <= lo)) {
-                H[k]++;
-                if (is_leaf(k) && lo > 0.001f) near = std::fmin(near, lo);
-                k = is_leaf(k) ? skip : k + 1;
-            } else {
-                k = skip;
-            }
-            if (k == RT_NODE_END) break;
-        }
-        return near;
-    };
     const int gx = 128, gy = 72;
-    uint32_t seed = 0x9E3779B9u;
-    auto unit = [&]() {   // xorshift32 in [0, 1)
-        seed ^= seed << 13;
-        seed ^= seed >> 17;
-        seed ^= seed << 5;
-        return (float)(seed >> 8) * (1.0f / 16777216.0f);
-    };
+    std::vector<int64_t> H(n, 0);
     for (int j = 0; j < gy; j++) {
         for (int i = 0; i < gx; i++) {
             const float px = ((float)i + 0.5f) * (float)width / (float)gx;
             const float py = ((float)j + 0.5f) * (float)height / (float)gy;
-            float o[3], d[3];
+            float o[3], inv[3];
             for (int k = 0; k < 3; k++) {
                 o[k] = cam.camera_pos[k];
-                d[k] = cam.up_left[k] + cam.pixel_delta_u[k] * px + cam.pixel_delta_v[k] * py - o[k];
+                const float d = cam.up_left[k] + cam.pixel_delta_u[k] * px + cam.pixel_delta_v[k] * py - o[k];
+                inv[k] = 1.0f / d;
             }
-            const float t = walk(o, d);
-            // mode 2: a bounce from where the camera ray enters its nearest leaf box, in a uniform
-            // direction -- a stand-in for the paths' later walks
-            if (mode == 2 && t < INFINITY) {
-                float p[3], e[3];
-                for (int k = 0; k < 3; k++) p[k] = o[k] + d[k] * t;
-                const float z = 2.0f * unit() - 1.0f, ph = 6.2831853f * unit(), r = std::sqrt(std::fmax(0.0f, 1.0f - z * z));
-                e[0] = r * std::cos(ph);
-                e[1] = r * std::sin(ph);
-                e[2] = z;
-                walk(p, e);
+            uint32_t k = 0;
+            while (k < n) {
+                const rt_dnode& b = dn[k];
+                const float lo3[3] = {b.xmin, b.ymin, b.zmin}, hi3[3] = {b.xmax, b.ymax, b.zmax};
+                float lo = 0.001f, hi = INFINITY;
+                for (int a = 0; a < 3; a++) {
+                    const float t0 = (lo3[a] - o[a]) * inv[a], t1 = (hi3[a] - o[a]) * inv[a];
+                    lo = std::fmax(lo, std::fmin(t0, t1));
+                    hi = std::fmin(hi, std::fmax(t0, t1));
+                }
+                const uint32_t skip = b.meta & 0xFFFFu;
+                if (!(hi <= lo)) {
+                    H[k]++;
+                    k = is_leaf(k) ? skip : k + 1;
+                } else {
+                    k = skip;
+                }
+                if (k == RT_NODE_END) break;
             }
         }
     }
@@ -685,7 +654,7 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
         memo.emplace(key, best);
         return best;
     };
-    std::vector<std::pair<uint32_t, int64_t>> st{{0u, walks}};
+    std::vector<std::pair<uint32_t, int64_t>> st{{0u, (int64_t)gx * gy}};
     while (!st.empty()) {
         const auto [k, v] = st.back();
         st.pop_back();
@@ -716,8 +685,7 @@ int walk_frac_for(int n_nodes) { return n_nodes <= RT_SMALL_TREE ? 8 : n_nodes <
 // it: for a ray starting inside all of them they are hits, tested on every walk (11 of
 // scene 8's ~41 node steps per walk).  Picks the longest prefix of the chain whose boxes'
 // intersection holds the camera and >= 3/4 of the leaf boxes' centres (where later walks
-// start), at least one node (the rebuilt trees' root, which holds scene 8's fog, is one); its
-// last node's hit successor is where such a walk starts.
+// start), at least 3 nodes; its last node's hit successor is where such a walk starts.
 void plan_spine(const std::vector<float4>& L, int n_nodes, const rt_camera_ubo& cam, bool on,
                 rt_kernel_args& a) {
     a.spine_len = 0;
@@ -769,7 +737,7 @@ void plan_spine(const std::vector<float4>& L, int n_nodes, const rt_camera_ubo& 
                   cx[3 * j + 2] > slo[2] && cx[3 * j + 2] < shi[2];
         if (4 * in < 3 * n_leaf) break;
         const uint32_t hit = bits(b1.z);
-        if (len >= 1) {
+        if (len >= 3) {
             a.spine_len = len;
             a.spine_start = hit;
             for (int k = 0; k < 3; k++) {
@@ -1977,17 +1945,17 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         const bool use_v = c->box_vnodes && all_cmp && a.box_margin > 0.0f && (c->variant == 0 || c->variant == 39) &&
                            c->boxc_host.size() == nb * RT_BOXC_F4;
         // node collapse (plan_collapse): planned for the camera, so rebuilt when it or the image size changes
-        const bool use_c = c->collapse > 0 && (c->variant == 0 || c->variant == 39) && c->have_cam;
+        const bool use_c = c->collapse && (c->variant == 0 || c->variant == 39) && c->have_cam;
         const bool cam_moved = use_c && (std::memcmp(&c->walk_cam, &c->cam, sizeof(rt_camera_ubo)) != 0 ||
                                          c->walk_w != c->width || c->walk_h != c->height);
         const bool use_r = c->rebuild && (c->variant == 0 || c->variant == 39);
         if (c->walk_stale || use_v != c->walk_v || (use_v && a.box_margin != c->walk_v_margin) ||
-            use_c != c->walk_c || cam_moved || use_r != c->walk_r || c->collapse != c->walk_cmode) {
+            use_c != c->walk_c || cam_moved || use_r != c->walk_r) {
             std::vector<rt_dnode> rb;
             if (use_r) rb = rebuild_inner(c->walk_dn);
             const std::vector<rt_dnode>& wdn = rb.empty() ? c->walk_dn : rb;
             std::vector<uint8_t> drop;
-            if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height, c->collapse);
+            if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height);
             c->n_dropped = 0;
             for (uint8_t x : drop) c->n_dropped += x;
             const std::vector<uint8_t>* dp = c->n_dropped ? &drop : nullptr;
@@ -2013,7 +1981,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                 c->n_walk_nodes = c->n_link_nodes;
             }
             c->walk_c = use_c;
-            c->walk_cmode = c->collapse;
             c->walk_r = use_r;
             c->n_rebuilt = rb.empty() ? 0 : (int)rb.size();
             c->walk_cam = c->cam;
@@ -2721,7 +2688,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SHADE_LDS: c->shade_lds = v != 0; break;
         case RT_OPTION_BOX_VNODES: c->box_vnodes = v != 0; break;
         case RT_OPTION_ZERO_DIR_END: c->zero_dir_end = v != 0; break;
-        case RT_OPTION_COLLAPSE: if (v < 0 || v > 2) return bad(); c->collapse = v; break;
+        case RT_OPTION_COLLAPSE: c->collapse = v != 0; break;
         case RT_OPTION_REBUILD: c->rebuild = v != 0; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
