@@ -634,39 +634,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             q2 = r[2];
         }
         unsigned long long c0 = STATS ? clock64() : 0;
-        // With the records prefetched, a sphere and a medium with a sphere boundary share one block:
-        // the boundary's quadratic is the sphere test's (hitting.glsl:17-38 twice, :165-168), so
-        // both roots are computed once for every such lane (sphere_roots: the same values and
-        // division form), then each type selects as its own code does -- the sphere its root in
-        // ray_t (sphere_t_ab), the medium its two boundary hits and the distance draw
-        // (sphere_bounds, medium_tail).  Where a wave holds both, one dependent chain instead of two.
-        const bool msph = pf && ty == RT_MODEL_CONSTANT_MEDIUM && __float_as_int(q0.y) == RT_MODEL_SPHERE;
-        if (pf && (ty == RT_MODEL_SPHERE || msph)) {
-            const float4 A = msph ? q1 : q0, B = msph ? q2 : q1;
-            float lo = 0.0f, hi = 0.0f;
-            const bool ok = sphere_roots(A, B, time, o, d, a, lo, hi, fd);
-            if (!msph) {
-                float root = lo;
-                hit = ok && tmin < root && root < tmax;
-                if (ok && !hit) {
-                    root = hi;
-                    hit = tmin < root && root < tmax;
-                }
-                t = root;
-                if (hit) { h.uv_kind_idx = (1 << 16) | ix; h.uv_a = t; }
-            } else {
-                const bool lo_in = -RT_INFINITY < lo && lo < RT_INFINITY;
-                const bool hi_in = -RT_INFINITY < hi && hi < RT_INFINITY;
-                const float t1 = lo_in ? lo : hi;
-                const float lo2 = t1 + 0.0001f;
-                const bool lo_2 = lo2 < lo && lo < RT_INFINITY;
-                const bool hi_2 = lo2 < hi && hi < RT_INFINITY;
-                const float t2 = lo_2 ? lo : hi;
-                hit = ok && (lo_in || hi_in) && (lo_2 || hi_2) &&
-                      medium_tail(q0.z, t1, t2, a, tmin, tmax, rf, px, py, t);
-            }
-            if (STATS) st_add(st, msph ? ST_MED_CYC : ST_SPH_CYC, clock64() - c0);
-        } else if (ty == RT_MODEL_SPHERE) {
+        if (ty == RT_MODEL_SPHERE) {
             if (pf) {
                 hit = sphere_t_ab(q0, q1, time, o, d, a, tmin, tmax, t, fd, fd ? rcp_nr(a) : 0.0f);
             } else if (P.sph_lds >= 0) {   // the record's intersection half from LDS (render_persistent)
