@@ -155,8 +155,11 @@ struct rt_ctx {
     bool box_vnodes = true;         // option box_vnodes
     bool zero_dir_end = true;       // option zero_dir_end (rt_kernel.hip render_stream)
     bool collapse = true;           // option collapse: the walk leaves out inner nodes (plan_collapse)
-    bool rebuild = true;            // option rebuild: the walk's inner nodes rebuilt over its leaves (rebuild_inner)
+    int rebuild = 1;                // option rebuild: the walk's inner nodes rebuilt over its leaves (rebuild_inner mode)
     bool walk_r = false;            // walk_links were built on the rebuilt inner nodes
+    int walk_rmode = 0;             // ... of this mode
+    std::vector<rt_dnode> rb_dn;    // rebuild_inner(walk_dn, rb_mode), kept across camera moves
+    int rb_mode = -1;               // -1: not built for the current walk_dn
     bool walk_c = false;            // walk_links were built with a collapse plan ...
     rt_camera_ubo walk_cam{};       // ... for this camera and image size
     int walk_w = 0, walk_h = 0;
@@ -514,7 +517,7 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
 // through 35% fewer node tests (tools/node_collapse_study.py).  Leaves and their records are
 // unchanged.  Empty when a leaf box is flat or inverted (plan_collapse's condition) or the
 // tree has fewer than 3 leaves.
-std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn) {
+std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn, int mode = 1) {
     std::vector<rt_dnode> out;
     const size_t n = dn.size();
     if (n <= RT_SMALL_TREE || n > RT_LINK_MAX_NODES) return out;
@@ -538,6 +541,36 @@ std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn) {
     };
     out.resize(2 * m - 1);
     std::vector<rt_dnode> pre(m), suf(m);
+    // mode 2 (up to 1024 leaves): the split points of the tree whose inner boxes' areas sum least,
+    // by a dynamic programme over the ranges (O(leaves^3)); otherwise each range split greedily
+    std::vector<uint32_t> split;
+    if (mode == 2 && m <= 1024) {
+        std::vector<double> A(m * m), C(m * m, 0.0);
+        for (size_t i = 0; i < m; i++) {
+            rt_dnode b = dn[L[i]];
+            for (size_t j = i; j < m; j++) {
+                if (j > i) join(b, dn[L[j]]);
+                A[i * m + j] = area(b);
+            }
+        }
+        split.assign(m * m, 0);
+        for (size_t len = 2; len <= m; len++) {
+            for (size_t i = 0; i + len <= m; i++) {
+                const size_t j = i + len - 1;
+                double best = INFINITY;
+                uint32_t bk = (uint32_t)i;
+                for (size_t k = i; k < j; k++) {
+                    const double c = C[i * m + k] + C[(k + 1) * m + j];
+                    if (c < best) {
+                        best = c;
+                        bk = (uint32_t)k;
+                    }
+                }
+                C[i * m + j] = A[i * m + j] + best;
+                split[i * m + j] = bk;
+            }
+        }
+    }
     // pre-order emission: (range, slot); a node's first child follows it, its skip is the slot
     // after its subtree (2 x leaves - 1 slots), RT_NODE_END past the last
     struct Item { uint32_t i, j, at; };
@@ -563,7 +596,11 @@ std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn) {
         }
         uint32_t best = 1;
         double best_c = INFINITY;
-        for (uint32_t s = 1; s < cnt; s++) {
+        if (!split.empty()) {
+            best = split[(size_t)it.i * m + (it.j - 1)] - it.i + 1;
+            best_c = 0.0;
+        }
+        for (uint32_t s = 1; s < cnt && split.empty(); s++) {
             const double cst = area(pre[s - 1]) * s + area(suf[s]) * (cnt - s);
             if (cst < best_c) {
                 best_c = cst;
@@ -1948,11 +1985,16 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         const bool use_c = c->collapse && (c->variant == 0 || c->variant == 39) && c->have_cam;
         const bool cam_moved = use_c && (std::memcmp(&c->walk_cam, &c->cam, sizeof(rt_camera_ubo)) != 0 ||
                                          c->walk_w != c->width || c->walk_h != c->height);
-        const bool use_r = c->rebuild && (c->variant == 0 || c->variant == 39);
+        const bool use_r = c->rebuild > 0 && (c->variant == 0 || c->variant == 39);
         if (c->walk_stale || use_v != c->walk_v || (use_v && a.box_margin != c->walk_v_margin) ||
-            use_c != c->walk_c || cam_moved || use_r != c->walk_r) {
-            std::vector<rt_dnode> rb;
-            if (use_r) rb = rebuild_inner(c->walk_dn);
+            use_c != c->walk_c || cam_moved || use_r != c->walk_r || c->rebuild != c->walk_rmode) {
+            if (c->walk_stale) c->rb_mode = -1;   // a new walk_dn (validate)
+            if (use_r && c->rb_mode != c->rebuild) {
+                c->rb_dn = rebuild_inner(c->walk_dn, c->rebuild);
+                c->rb_mode = c->rebuild;
+            }
+            static const std::vector<rt_dnode> none;
+            const std::vector<rt_dnode>& rb = use_r ? c->rb_dn : none;
             const std::vector<rt_dnode>& wdn = rb.empty() ? c->walk_dn : rb;
             std::vector<uint8_t> drop;
             if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height);
@@ -1982,6 +2024,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             }
             c->walk_c = use_c;
             c->walk_r = use_r;
+            c->walk_rmode = c->rebuild;
             c->n_rebuilt = rb.empty() ? 0 : (int)rb.size();
             c->walk_cam = c->cam;
             c->walk_w = c->width;
@@ -2523,7 +2566,7 @@ int rt_debug_collapse_links(const void* bvh, size_t nbytes, const float cam[28],
     int r = thread_bvh(&tmp, (const rt_bvh_node*)bvh, (int)(nbytes / sizeof(rt_bvh_node)), dn);
     if (r) return r;
     if (rebuild) {
-        std::vector<rt_dnode> rb = rebuild_inner(dn);
+        std::vector<rt_dnode> rb = rebuild_inner(dn, rebuild);
         if (!rb.empty()) dn.swap(rb);
     }
     rt_camera_ubo cu;
@@ -2689,7 +2732,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_BOX_VNODES: c->box_vnodes = v != 0; break;
         case RT_OPTION_ZERO_DIR_END: c->zero_dir_end = v != 0; break;
         case RT_OPTION_COLLAPSE: c->collapse = v != 0; break;
-        case RT_OPTION_REBUILD: c->rebuild = v != 0; break;
+        case RT_OPTION_REBUILD: if (v < 0 || v > 2) return bad(); c->rebuild = v; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
         case RT_OPTION_STAGE_TILES: if (v < 0) return bad(); c->stage_tiles = v; break;
