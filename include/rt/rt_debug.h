@@ -138,12 +138,14 @@ enum {
                                            miss colour its next bounce would give (1)       */
     RT_OPTION_COLLAPSE = 25,            /* the link walk leaves out the inner nodes whose
                                            tests a grid of camera rays says cost more than
-                                           they save (boxes nest: the same leaves, order
-                                           and ray_t; rt_capi.hip plan_collapse) (1)       */
+                                           they save (rt_capi.hip plan_collapse): 1 the rays
+                                           pass every prim (default), 2 they stop at their
+                                           solid hits; 0 off                                */
     RT_OPTION_REBUILD = 26,             /* the link walk's inner nodes rebuilt over the
-                                           reference's leaf sequence (surface-area splits,
-                                           joined boxes: the same leaves, order and ray_t;
-                                           rt_capi.hip rebuild_inner) (1)                   */
+                                           reference's leaf sequence (joined boxes: the same
+                                           leaves, order and ray_t; rt_capi.hip
+                                           rebuild_inner): 1 greedy surface-area splits,
+                                           2 the least summed inner-box area (default); 0 off */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

@@ -154,10 +154,11 @@ struct rt_ctx {
     std::vector<float4> boxc_host;  // the compact box records (host copy of Device::dboxc)
     bool box_vnodes = true;         // option box_vnodes
     bool zero_dir_end = true;       // option zero_dir_end (rt_kernel.hip render_stream)
-    bool collapse = true;           // option collapse: the walk leaves out inner nodes (plan_collapse)
-    int rebuild = 1;                // option rebuild: the walk's inner nodes rebuilt over its leaves (rebuild_inner mode)
+    int collapse = 1;               // option collapse: the walk leaves out inner nodes (plan_collapse; 2: grid rays stop at their solid hits)
+    int rebuild = 2;                // option rebuild: the walk's inner nodes rebuilt over its leaves (rebuild_inner mode)
     bool walk_r = false;            // walk_links were built on the rebuilt inner nodes
     int walk_rmode = 0;             // ... of this mode
+    int walk_cmode = 0;             // the collapse mode walk_links were planned with
     std::vector<rt_dnode> rb_dn;    // rebuild_inner(walk_dn, rb_mode), kept across camera moves
     int rb_mode = -1;               // -1: not built for the current walk_dn
     bool walk_c = false;            // walk_links were built with a collapse plan ...
@@ -541,11 +542,11 @@ std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn, int mode = 
     };
     out.resize(2 * m - 1);
     std::vector<rt_dnode> pre(m), suf(m);
-    // mode 2 (up to 1024 leaves): the split points of the tree whose inner boxes' areas sum least,
-    // by a dynamic programme over the ranges (O(leaves^3)); otherwise each range split greedily
+    // mode 2 (up to 4096 leaves): the split points of the tree whose inner boxes' areas sum least,
+    // by a dynamic programme over the ranges; otherwise each range split greedily
     std::vector<uint32_t> split;
-    if (mode == 2 && m <= 1024) {
-        std::vector<double> A(m * m), C(m * m, 0.0);
+    if (mode == 2 && m <= 4096) {
+        std::vector<double> A(m * m), C(m * m, 0.0), CT(m * m, 0.0);   // CT[j * m + i] = C[i * m + j]
         for (size_t i = 0; i < m; i++) {
             rt_dnode b = dn[L[i]];
             for (size_t j = i; j < m; j++) {
@@ -559,14 +560,28 @@ std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn, int mode = 
                 const size_t j = i + len - 1;
                 double best = INFINITY;
                 uint32_t bk = (uint32_t)i;
-                for (size_t k = i; k < j; k++) {
-                    const double c = C[i * m + k] + C[(k + 1) * m + j];
+                const double* row = &C[i * m];
+                const double* col = &CT[j * m + 1];   // col[k] = C[(k + 1) * m + j]
+                // Knuth's window: the best split of [i, j] between those of [i, j - 1] and [i + 1, j]
+                // (exact when the costs satisfy the quadrangle inequality; any split is exact for the
+                // walk, so a window that misses the optimum only costs node tests): O(leaves^2)
+                size_t k0 = i, k1 = j - 1;
+                if (len > 2) {
+                    k0 = std::max<size_t>(i, split[i * m + j - 1]);
+                    k1 = std::min<size_t>(j - 1, split[(i + 1) * m + j]);
+                    if (k0 > k1) {
+                        k0 = i;
+                        k1 = j - 1;
+                    }
+                }
+                for (size_t k = k0; k <= k1; k++) {
+                    const double c = row[k] + col[k];
                     if (c < best) {
                         best = c;
                         bk = (uint32_t)k;
                     }
                 }
-                C[i * m + j] = A[i * m + j] + best;
+                C[i * m + j] = CT[j * m + i] = A[i * m + j] + best;
                 split[i * m + j] = bk;
             }
         }
@@ -634,7 +649,78 @@ std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn, int mode = 
 // counts taken by a dynamic programme over the tree; the root stays (the walk starts there).
 // tools/node_collapse_study.py: on scene 8 this grid's choice cuts the node tests of the
 // reference's own walks by 11.5% beyond the spine (the best choice for the walks themselves: 16%).
-std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height) {
+// The grid rays' solid hits for plan_collapse mode 2 (a heuristic: host floats, a sphere at its
+// time-0 centre, media passed through): the nearest t in (tmin, tmax) of prim `ix` of type `ty`.
+struct PrimRecs {
+    const rt_sphere* sph = nullptr;
+    size_t ns = 0;
+    const rt_quad* quad = nullptr;
+    size_t nq = 0;
+    const rt_box* box = nullptr;
+    size_t nb = 0;
+};
+static bool host_quad_t(const rt_quad& q, const float o[3], const float d[3], float tmin, float tmax, float& t) {
+    const float* n = q.normal;
+    const float den = n[0] * d[0] + n[1] * d[1] + n[2] * d[2];
+    if (std::fabs(den) < 1e-8f) return false;
+    const float tt = (q.d - (n[0] * o[0] + n[1] * o[1] + n[2] * o[2])) / den;
+    if (!(tmin <= tt && tt <= tmax)) return false;
+    float p[3], cx[3];
+    for (int a = 0; a < 3; a++) p[a] = o[a] + d[a] * tt - q.q[a];
+    const float* u = q.u;
+    const float* v = q.v;
+    cx[0] = u[1] * v[2] - u[2] * v[1];
+    cx[1] = u[2] * v[0] - u[0] * v[2];
+    cx[2] = u[0] * v[1] - u[1] * v[0];
+    const float nn = cx[0] * cx[0] + cx[1] * cx[1] + cx[2] * cx[2];
+    if (!(nn > 0.0f)) return false;
+    auto trip = [&](const float* a, const float* b) {   // dot(w, cross(a, b)), w = cross(u, v) / |cross(u, v)|^2
+        const float c0 = a[1] * b[2] - a[2] * b[1], c1 = a[2] * b[0] - a[0] * b[2], c2 = a[0] * b[1] - a[1] * b[0];
+        return (cx[0] * c0 + cx[1] * c1 + cx[2] * c2) / nn;
+    };
+    const float al = trip(p, v), be = trip(u, p);
+    if (!(al >= 0.0f && al <= 1.0f && be >= 0.0f && be <= 1.0f)) return false;
+    t = tt;
+    return true;
+}
+static bool host_prim_t(const PrimRecs& R, uint32_t ty, uint32_t ix, const float o[3], const float d[3], float tmin,
+                        float tmax, float& t) {
+    if (ty == RT_MODEL_SPHERE && ix < R.ns) {
+        const rt_sphere& s = R.sph[ix];
+        float oc[3];
+        for (int a = 0; a < 3; a++) oc[a] = o[a] - s.center1[a];
+        const float aa = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        const float hb = oc[0] * d[0] + oc[1] * d[1] + oc[2] * d[2];
+        const float cc = oc[0] * oc[0] + oc[1] * oc[1] + oc[2] * oc[2] - s.radius * s.radius;
+        const float disc = hb * hb - aa * cc;
+        if (!(disc >= 0.0f) || !(aa > 0.0f)) return false;
+        const float sq = std::sqrt(disc);
+        float r = (-hb - sq) / aa;
+        if (!(tmin < r && r < tmax)) {
+            r = (-hb + sq) / aa;
+            if (!(tmin < r && r < tmax)) return false;
+        }
+        t = r;
+        return true;
+    }
+    if (ty == RT_MODEL_QUAD && ix < R.nq) return host_quad_t(R.quad[ix], o, d, tmin, tmax, t);
+    if (ty == RT_MODEL_BOX && ix < R.nb) {
+        bool hit = false;
+        for (int f = 0; f < 6; f++) {
+            float tf;
+            if (host_quad_t(R.box[ix].quads[f], o, d, tmin, tmax, tf)) {
+                tmax = tf;
+                t = tf;
+                hit = true;
+            }
+        }
+        return hit;
+    }
+    return false;
+}
+
+std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height,
+                                   const PrimRecs* prims = nullptr) {
     const size_t n = dn.size();
     std::vector<uint8_t> drop(n, 0);
     if (n <= RT_SMALL_TREE || n > RT_LINK_MAX_NODES || width <= 0 || height <= 0 || !boxes_nest(dn)) return drop;
@@ -647,17 +733,18 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
         for (int i = 0; i < gx; i++) {
             const float px = ((float)i + 0.5f) * (float)width / (float)gx;
             const float py = ((float)j + 0.5f) * (float)height / (float)gy;
-            float o[3], inv[3];
+            float o[3], inv[3], dv[3];
             for (int k = 0; k < 3; k++) {
                 o[k] = cam.camera_pos[k];
-                const float d = cam.up_left[k] + cam.pixel_delta_u[k] * px + cam.pixel_delta_v[k] * py - o[k];
-                inv[k] = 1.0f / d;
+                dv[k] = cam.up_left[k] + cam.pixel_delta_u[k] * px + cam.pixel_delta_v[k] * py - o[k];
+                inv[k] = 1.0f / dv[k];
             }
             uint32_t k = 0;
+            float tmax = INFINITY;
             while (k < n) {
                 const rt_dnode& b = dn[k];
                 const float lo3[3] = {b.xmin, b.ymin, b.zmin}, hi3[3] = {b.xmax, b.ymax, b.zmax};
-                float lo = 0.001f, hi = INFINITY;
+                float lo = 0.001f, hi = tmax;
                 for (int a = 0; a < 3; a++) {
                     const float t0 = (lo3[a] - o[a]) * inv[a], t1 = (hi3[a] - o[a]) * inv[a];
                     lo = std::fmax(lo, std::fmin(t0, t1));
@@ -666,6 +753,13 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
                 const uint32_t skip = b.meta & 0xFFFFu;
                 if (!(hi <= lo)) {
                     H[k]++;
+                    if (is_leaf(k) && prims) {   // mode 2: the leaf's solid prims shrink ray_t.max
+                        for (int sl = 0; sl < 2; sl++) {
+                            const uint32_t ty = (b.meta >> (16 + 4 * sl)) & 0xFu, ix = (b.prims >> (16 * sl)) & 0xFFFFu;
+                            float th;
+                            if (ty && host_prim_t(*prims, ty, ix, o, dv, 0.001f, tmax, th)) tmax = th;
+                        }
+                    }
                     k = is_leaf(k) ? skip : k + 1;
                 } else {
                     k = skip;
@@ -1982,12 +2076,13 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         const bool use_v = c->box_vnodes && all_cmp && a.box_margin > 0.0f && (c->variant == 0 || c->variant == 39) &&
                            c->boxc_host.size() == nb * RT_BOXC_F4;
         // node collapse (plan_collapse): planned for the camera, so rebuilt when it or the image size changes
-        const bool use_c = c->collapse && (c->variant == 0 || c->variant == 39) && c->have_cam;
+        const bool use_c = c->collapse > 0 && (c->variant == 0 || c->variant == 39) && c->have_cam;
         const bool cam_moved = use_c && (std::memcmp(&c->walk_cam, &c->cam, sizeof(rt_camera_ubo)) != 0 ||
                                          c->walk_w != c->width || c->walk_h != c->height);
         const bool use_r = c->rebuild > 0 && (c->variant == 0 || c->variant == 39);
         if (c->walk_stale || use_v != c->walk_v || (use_v && a.box_margin != c->walk_v_margin) ||
-            use_c != c->walk_c || cam_moved || use_r != c->walk_r || c->rebuild != c->walk_rmode) {
+            use_c != c->walk_c || cam_moved || use_r != c->walk_r || c->rebuild != c->walk_rmode ||
+            c->collapse != c->walk_cmode) {
             if (c->walk_stale) c->rb_mode = -1;   // a new walk_dn (validate)
             if (use_r && c->rb_mode != c->rebuild) {
                 c->rb_dn = rebuild_inner(c->walk_dn, c->rebuild);
@@ -1997,7 +2092,19 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             const std::vector<rt_dnode>& rb = use_r ? c->rb_dn : none;
             const std::vector<rt_dnode>& wdn = rb.empty() ? c->walk_dn : rb;
             std::vector<uint8_t> drop;
-            if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height);
+            PrimRecs pr;
+            if (c->collapse == 2) {
+                const std::vector<uint8_t>& SB = c->host_buf[RT_BIND_SPHERES];
+                const std::vector<uint8_t>& QB = c->host_buf[RT_BIND_QUADS];
+                const std::vector<uint8_t>& BB = c->host_buf[RT_BIND_BOXES];
+                pr.sph = (const rt_sphere*)SB.data();
+                pr.ns = SB.size() / sizeof(rt_sphere);
+                pr.quad = (const rt_quad*)QB.data();
+                pr.nq = QB.size() / sizeof(rt_quad);
+                pr.box = (const rt_box*)BB.data();
+                pr.nb = BB.size() / sizeof(rt_box);
+            }
+            if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height, c->collapse == 2 ? &pr : nullptr);
             c->n_dropped = 0;
             for (uint8_t x : drop) c->n_dropped += x;
             const std::vector<uint8_t>* dp = c->n_dropped ? &drop : nullptr;
@@ -2023,6 +2130,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                 c->n_walk_nodes = c->n_link_nodes;
             }
             c->walk_c = use_c;
+            c->walk_cmode = c->collapse;
             c->walk_r = use_r;
             c->walk_rmode = c->rebuild;
             c->n_rebuilt = rb.empty() ? 0 : (int)rb.size();
@@ -2731,7 +2839,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SHADE_LDS: c->shade_lds = v != 0; break;
         case RT_OPTION_BOX_VNODES: c->box_vnodes = v != 0; break;
         case RT_OPTION_ZERO_DIR_END: c->zero_dir_end = v != 0; break;
-        case RT_OPTION_COLLAPSE: c->collapse = v != 0; break;
+        case RT_OPTION_COLLAPSE: if (v < 0 || v > 2) return bad(); c->collapse = v; break;
         case RT_OPTION_REBUILD: if (v < 0 || v > 2) return bad(); c->rebuild = v; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;

@@ -232,7 +232,7 @@ def test_collapsed_walk_matches_oracle_and_follows_the_camera(gpu):
         ctx.render(1, rtamd.frame_rand_factors(1, 0, 4))
         out = ctx.read_image()
         info = ctx.last_launch()
-        _, _, nd = collapse_links(s, 48, 27, rebuild=1)
+        _, _, nd = collapse_links(s, 48, 27, rebuild=2)
         assert info["collapsed"] == nd > 0, (info, nd)
         ref = oracle_image(s, 4, max_depth=5)
         assert bit_equal(out, ref), mismatch_report(out, ref)

@@ -398,9 +398,11 @@ def walk_links_rays(ln, n, o, d, inv, exact):
     return tested
 
 
+@pytest.mark.parametrize("rebuild", [1, 2])
 @pytest.mark.parametrize("sid", [8, 0, 6])
-def test_rebuilt_inner_nodes_test_the_same_leaves(sid):
-    """The inner nodes rebuilt over the reference's leaf sequence (option rebuild), then collapsed
+def test_rebuilt_inner_nodes_test_the_same_leaves(sid, rebuild):
+    """The inner nodes rebuilt over the reference's leaf sequence (option rebuild: 1 greedy surface-area
+    splits, 2 the least summed inner-box area by a dynamic programme), then collapsed
     (option collapse): for rays through the scene -- some with a zero direction component (1/dir
     = +-inf), ray_t.max shrinking at some leaves -- the walk over the links tests the reference
     tree's leaves in the same order under the same ray_t.max.  Nothing about the inner nodes
@@ -408,7 +410,7 @@ def test_rebuilt_inner_nodes_test_the_same_leaves(sid):
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
     tn = threaded(scene)
     n = len(tn)
-    ln, drop, nd = collapse_links(scene, rebuild=1)
+    ln, drop, nd = collapse_links(scene, rebuild=rebuild)
     leaves_tn = [(int(x["meta"]) >> 16 & 0xFF, int(x["prims"])) for x in tn if is_leaf(x)]
     w = ln.view(np.uint32)
     rec = [(int(a) & 0xFF, int(b)) for a, b in w[2 * n:].reshape(-1, 2)][:len(leaves_tn)]
