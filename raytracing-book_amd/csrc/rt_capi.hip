@@ -166,6 +166,7 @@ struct rt_ctx {
     int walk_w = 0, walk_h = 0;
     int n_dropped = 0;              // inner nodes the walk leaves out
     int n_rebuilt = 0;              // nodes of the rebuilt tree (0: the tree as uploaded / built)
+    int n_vnodes = 0;               // box pre-test nodes in walk_links
     FastTables fast;
     std::vector<float4> links;   // build_links(dnodes), empty when unavailable
     int fast_gen = 0;
@@ -411,7 +412,8 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
     if (n == 0 || n > RT_LINK_MAX_NODES) return out;
     auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
     // Node collapse (plan_collapse): a link that leads to a left-out inner node leads to its first
-    // child (threaded k + 1) instead, repeatedly; the left-out nodes keep their place, unreachable.
+    // child (threaded k + 1) instead, repeatedly; the left-out nodes get no place (the kept nodes keep
+    // their breadth-first order, so a two-level launch's LDS prefix holds only reachable nodes).
     const bool dropping = drop && drop->size() == n && !(*drop)[0];
     auto kept = [&](uint32_t k) {
         while (dropping && k < n && (*drop)[k] && !is_leaf(k)) k++;
@@ -431,6 +433,14 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
         order.push_back(l);
     }
     if (order.size() != n) return out;
+    size_t nk = n;   // the tree's nodes that get a place
+    if (dropping) {
+        nk = 0;
+        for (size_t h = 0; h < n; h++) {
+            const uint32_t k = order[h];
+            pos[k] = ((*drop)[k] && !is_leaf(k)) ? 0xFFFFFFFFu : (uint32_t)nk++;
+        }
+    }
     // Box pre-tests as nodes (vbox: 6 floats per box, its bounds grown by the pre-test's margin,
     // rt_kernel.hip leaf_prims_t): a leaf of one or two boxes becomes a chain of one node per box
     // whose hit leads to that box's own leaf record -- the box tested alone, marked pre-tested
@@ -448,10 +458,10 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
         const uint32_t t0 = (dn[k].meta >> 16) & 0xFu, t1 = (dn[k].meta >> 20) & 0xFu;
         const uint32_t p0 = dn[k].prims & 0xFFFFu, p1 = dn[k].prims >> 16;
         if (t0 != RT_MODEL_BOX || (t1 != RT_MODEL_BOX && t1 != 0) || p0 >= nbox || (t1 && p1 >= nbox)) continue;
-        vfirst[k] = (uint32_t)(n + nv);
+        vfirst[k] = (uint32_t)(nk + nv);
         nv += t1 ? 2 : 1;
     }
-    const size_t N = n + nv;
+    const size_t N = nk + nv;
     if (N > RT_LINK_MAX_NODES) return build_links(dn, nullptr, n_nodes_out, drop);
     size_t nl = 0;
     for (size_t k = 0; k < n; k++)
@@ -470,6 +480,7 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
     uint32_t li = 0;
     for (size_t k = 0; k < n; k++) {
         const rt_dnode& d = dn[k];
+        if (pos[k] == 0xFFFFFFFFu) continue;   // left out (collapse)
         const uint32_t skip = d.meta & 0xFFFFu;
         const uint32_t skip_at = skip == RT_NODE_END ? RT_LINK_END : 32u * pos[kept(skip)];
         const uint32_t next_end = skip == RT_NODE_END ? RT_LINK_NEXT_END : skip_at;
@@ -2121,6 +2132,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                 int nn = 0;
                 c->walk_links = build_links(wdn, &vb, &nn, dp);
                 c->n_walk_nodes = nn;
+                c->n_vnodes = std::max(0, nn - ((int)wdn.size() - (dp ? c->n_dropped : 0)));
             } else if (dp || !rb.empty()) {
                 int nn = 0;
                 c->walk_links = build_links(wdn, nullptr, &nn, dp);
@@ -2129,6 +2141,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
                 c->walk_links = c->links;
                 c->n_walk_nodes = c->n_link_nodes;
             }
+            if (!use_v) c->n_vnodes = 0;
             c->walk_c = use_c;
             c->walk_cmode = c->collapse;
             c->walk_r = use_r;
@@ -2143,7 +2156,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             c->pair_leaves = -1;
             c->fast_gen++;   // re-upload the links (rt_render's device loop)
         }
-        a.box_vnodes = c->walk_v && c->n_walk_nodes > c->n_link_nodes ? 1 : 0;
+        a.box_vnodes = c->walk_v && c->n_vnodes > 0 ? 1 : 0;
     }
     a.n_nodes = c->n_walk_nodes;
     a.n_lnode_f4 = (int)c->walk_links.size();
@@ -2442,7 +2455,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             HIPCHK(c, hipEventRecord(d.ring_ev[slot], d.stream));
             if (&d == &c->devs[0]) {
                 c->last_launch[RT_LI_BVH_MODE] = c->bvh_mode;
-                c->last_launch[RT_LI_VNODES] = a.box_vnodes ? c->n_walk_nodes - c->n_link_nodes : 0;
+                c->last_launch[RT_LI_VNODES] = a.box_vnodes ? c->n_vnodes : 0;
                 c->last_launch[RT_LI_COLLAPSED] = c->walk_c ? c->n_dropped : 0;
                 c->last_launch[RT_LI_REBUILT] = c->n_rebuilt > 0 ? 1 : 0;
             }

@@ -289,21 +289,25 @@ def nested_hits(tn, rng, p):
 def test_collapsed_walk_tests_the_same_leaves(sid):
     """Leaving out inner nodes (option collapse): under every nested pattern of box hits the walk
     over the collapsed links tests the threaded walk's leaves in the same order, with fewer or more
-    node tests.  The links keep the tree's layout (the left-out nodes keep their places,
-    unreachable); the root and the leaf nodes are never left out."""
+    node tests.  The kept nodes keep their breadth-first order and boxes, the left-out ones get no
+    place; the root and the leaf nodes are never left out."""
     scene = rtamd.Scene(sid, 1920, 1080, seed=1)
     tn = threaded(scene)
     n = len(tn)
     ln, drop, nd = collapse_links(scene)
     plain = links_of(scene.buffers[1])
-    order = check_layout(tn, plain)
-    assert len(ln) == len(plain) and nd == int(drop.sum())
-    assert np.array_equal(ln[:2 * n].reshape(n, 8)[:, :6].view(np.uint32), plain[:2 * n].reshape(n, 8)[:, :6].view(np.uint32))
+    check_layout(tn, plain)
+    assert nd == int(drop.sum())
     assert drop[0] == 0 and not any(drop[k] for k in range(n) if is_leaf(tn[k]))
+    order = [k for k in bfs_order(tn) if not drop[k]]
+    nk = len(order)
+    n_leaves = sum(is_leaf(x) for x in tn)
+    assert nk == n - nd and len(ln) == 2 * nk + (n_leaves + 1) // 2
+    assert np.array_equal(ln[:2 * nk].reshape(nk, 8)[:, :6].view(np.uint32),
+                          np.stack([tn[k]["box"] for k in order]).view(np.uint32))
+    n = nk
     if sid == 8:
         assert nd > 100   # the fog's chain and much of the sphere cluster's upper levels
-    pos = np.empty(n, np.int64)
-    pos[order] = np.arange(n)
     rng = np.random.default_rng(200 + sid)
     steps_full = steps_coll = 0
     for p in (0.3, 0.6, 0.9, 1.0):
@@ -411,9 +415,11 @@ def test_rebuilt_inner_nodes_test_the_same_leaves(sid, rebuild):
     tn = threaded(scene)
     n = len(tn)
     ln, drop, nd = collapse_links(scene, rebuild=rebuild)
+    nk = n - nd   # the nodes with a place in the links (left-out ones have none)
     leaves_tn = [(int(x["meta"]) >> 16 & 0xFF, int(x["prims"])) for x in tn if is_leaf(x)]
     w = ln.view(np.uint32)
-    rec = [(int(a) & 0xFF, int(b)) for a, b in w[2 * n:].reshape(-1, 2)][:len(leaves_tn)]
+    assert len(ln) == 2 * nk + (len(leaves_tn) + 1) // 2
+    rec = [(int(a) & 0xFF, int(b)) for a, b in w[2 * nk:].reshape(-1, 2)][:len(leaves_tn)]
     assert rec == leaves_tn   # the same leaf records, in the same order
     boxes = np.stack([x["box"] for x in tn])
     lo, hi = boxes[0, 0::2], boxes[0, 1::2]
@@ -432,7 +438,7 @@ def test_rebuilt_inner_nodes_test_the_same_leaves(sid, rebuild):
             inv = (np.float32(1.0) / d).astype(np.float32)
             exact = bool(np.any(inv == -np.inf))
             want = walk_tree_rays(tn, o, d, inv, exact)
-            got = walk_links_rays(ln, n, o, d, inv, exact)
+            got = walk_links_rays(ln, nk, o, d, inv, exact)
         assert got == want, (r, o, d)
         differ += len(want) > 0
     assert differ > 50
