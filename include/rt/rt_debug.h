@@ -138,9 +138,7 @@ enum {
                                            miss colour its next bounce would give (1)       */
     RT_OPTION_COLLAPSE = 25,            /* the link walk leaves out the inner nodes whose
                                            tests a grid of camera rays says cost more than
-                                           they save (rt_capi.hip plan_collapse): 1 the rays
-                                           pass every prim (default), 2 they stop at their
-                                           solid hits; 0 off                                */
+                                           they save (rt_capi.hip plan_collapse) (1)        */
     RT_OPTION_REBUILD = 26,             /* the link walk's inner nodes rebuilt over the
                                            reference's leaf sequence (joined boxes: the same
                                            leaves, order and ray_t; rt_capi.hip

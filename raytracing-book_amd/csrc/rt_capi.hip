@@ -154,11 +154,10 @@ struct rt_ctx {
     std::vector<float4> boxc_host;  // the compact box records (host copy of Device::dboxc)
     bool box_vnodes = true;         // option box_vnodes
     bool zero_dir_end = true;       // option zero_dir_end (rt_kernel.hip render_stream)
-    int collapse = 1;               // option collapse: the walk leaves out inner nodes (plan_collapse; 2: grid rays stop at their solid hits)
+    bool collapse = true;           // option collapse: the walk leaves out inner nodes (plan_collapse)
     int rebuild = 2;                // option rebuild: the walk's inner nodes rebuilt over its leaves (rebuild_inner mode)
     bool walk_r = false;            // walk_links were built on the rebuilt inner nodes
     int walk_rmode = 0;             // ... of this mode
-    int walk_cmode = 0;             // the collapse mode walk_links were planned with
     std::vector<rt_dnode> rb_dn;    // rebuild_inner(walk_dn, rb_mode), kept across camera moves
     int rb_mode = -1;               // -1: not built for the current walk_dn
     bool walk_c = false;            // walk_links were built with a collapse plan ...
@@ -660,78 +659,7 @@ std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn, int mode = 
 // counts taken by a dynamic programme over the tree; the root stays (the walk starts there).
 // tools/node_collapse_study.py: on scene 8 this grid's choice cuts the node tests of the
 // reference's own walks by 11.5% beyond the spine (the best choice for the walks themselves: 16%).
-// The grid rays' solid hits for plan_collapse mode 2 (a heuristic: host floats, a sphere at its
-// time-0 centre, media passed through): the nearest t in (tmin, tmax) of prim `ix` of type `ty`.
-struct PrimRecs {
-    const rt_sphere* sph = nullptr;
-    size_t ns = 0;
-    const rt_quad* quad = nullptr;
-    size_t nq = 0;
-    const rt_box* box = nullptr;
-    size_t nb = 0;
-};
-static bool host_quad_t(const rt_quad& q, const float o[3], const float d[3], float tmin, float tmax, float& t) {
-    const float* n = q.normal;
-    const float den = n[0] * d[0] + n[1] * d[1] + n[2] * d[2];
-    if (std::fabs(den) < 1e-8f) return false;
-    const float tt = (q.d - (n[0] * o[0] + n[1] * o[1] + n[2] * o[2])) / den;
-    if (!(tmin <= tt && tt <= tmax)) return false;
-    float p[3], cx[3];
-    for (int a = 0; a < 3; a++) p[a] = o[a] + d[a] * tt - q.q[a];
-    const float* u = q.u;
-    const float* v = q.v;
-    cx[0] = u[1] * v[2] - u[2] * v[1];
-    cx[1] = u[2] * v[0] - u[0] * v[2];
-    cx[2] = u[0] * v[1] - u[1] * v[0];
-    const float nn = cx[0] * cx[0] + cx[1] * cx[1] + cx[2] * cx[2];
-    if (!(nn > 0.0f)) return false;
-    auto trip = [&](const float* a, const float* b) {   // dot(w, cross(a, b)), w = cross(u, v) / |cross(u, v)|^2
-        const float c0 = a[1] * b[2] - a[2] * b[1], c1 = a[2] * b[0] - a[0] * b[2], c2 = a[0] * b[1] - a[1] * b[0];
-        return (cx[0] * c0 + cx[1] * c1 + cx[2] * c2) / nn;
-    };
-    const float al = trip(p, v), be = trip(u, p);
-    if (!(al >= 0.0f && al <= 1.0f && be >= 0.0f && be <= 1.0f)) return false;
-    t = tt;
-    return true;
-}
-static bool host_prim_t(const PrimRecs& R, uint32_t ty, uint32_t ix, const float o[3], const float d[3], float tmin,
-                        float tmax, float& t) {
-    if (ty == RT_MODEL_SPHERE && ix < R.ns) {
-        const rt_sphere& s = R.sph[ix];
-        float oc[3];
-        for (int a = 0; a < 3; a++) oc[a] = o[a] - s.center1[a];
-        const float aa = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
-        const float hb = oc[0] * d[0] + oc[1] * d[1] + oc[2] * d[2];
-        const float cc = oc[0] * oc[0] + oc[1] * oc[1] + oc[2] * oc[2] - s.radius * s.radius;
-        const float disc = hb * hb - aa * cc;
-        if (!(disc >= 0.0f) || !(aa > 0.0f)) return false;
-        const float sq = std::sqrt(disc);
-        float r = (-hb - sq) / aa;
-        if (!(tmin < r && r < tmax)) {
-            r = (-hb + sq) / aa;
-            if (!(tmin < r && r < tmax)) return false;
-        }
-        t = r;
-        return true;
-    }
-    if (ty == RT_MODEL_QUAD && ix < R.nq) return host_quad_t(R.quad[ix], o, d, tmin, tmax, t);
-    if (ty == RT_MODEL_BOX && ix < R.nb) {
-        bool hit = false;
-        for (int f = 0; f < 6; f++) {
-            float tf;
-            if (host_quad_t(R.box[ix].quads[f], o, d, tmin, tmax, tf)) {
-                tmax = tf;
-                t = tf;
-                hit = true;
-            }
-        }
-        return hit;
-    }
-    return false;
-}
-
-std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height,
-                                   const PrimRecs* prims = nullptr) {
+std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height) {
     const size_t n = dn.size();
     std::vector<uint8_t> drop(n, 0);
     if (n <= RT_SMALL_TREE || n > RT_LINK_MAX_NODES || width <= 0 || height <= 0 || !boxes_nest(dn)) return drop;
@@ -744,18 +672,16 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
         for (int i = 0; i < gx; i++) {
             const float px = ((float)i + 0.5f) * (float)width / (float)gx;
             const float py = ((float)j + 0.5f) * (float)height / (float)gy;
-            float o[3], inv[3], dv[3];
+            float o[3], inv[3];
             for (int k = 0; k < 3; k++) {
                 o[k] = cam.camera_pos[k];
-                dv[k] = cam.up_left[k] + cam.pixel_delta_u[k] * px + cam.pixel_delta_v[k] * py - o[k];
-                inv[k] = 1.0f / dv[k];
+                inv[k] = 1.0f / (cam.up_left[k] + cam.pixel_delta_u[k] * px + cam.pixel_delta_v[k] * py - o[k]);
             }
             uint32_t k = 0;
-            float tmax = INFINITY;
             while (k < n) {
                 const rt_dnode& b = dn[k];
                 const float lo3[3] = {b.xmin, b.ymin, b.zmin}, hi3[3] = {b.xmax, b.ymax, b.zmax};
-                float lo = 0.001f, hi = tmax;
+                float lo = 0.001f, hi = INFINITY;
                 for (int a = 0; a < 3; a++) {
                     const float t0 = (lo3[a] - o[a]) * inv[a], t1 = (hi3[a] - o[a]) * inv[a];
                     lo = std::fmax(lo, std::fmin(t0, t1));
@@ -764,13 +690,6 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
                 const uint32_t skip = b.meta & 0xFFFFu;
                 if (!(hi <= lo)) {
                     H[k]++;
-                    if (is_leaf(k) && prims) {   // mode 2: the leaf's solid prims shrink ray_t.max
-                        for (int sl = 0; sl < 2; sl++) {
-                            const uint32_t ty = (b.meta >> (16 + 4 * sl)) & 0xFu, ix = (b.prims >> (16 * sl)) & 0xFFFFu;
-                            float th;
-                            if (ty && host_prim_t(*prims, ty, ix, o, dv, 0.001f, tmax, th)) tmax = th;
-                        }
-                    }
                     k = is_leaf(k) ? skip : k + 1;
                 } else {
                     k = skip;
@@ -2087,13 +2006,12 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         const bool use_v = c->box_vnodes && all_cmp && a.box_margin > 0.0f && (c->variant == 0 || c->variant == 39) &&
                            c->boxc_host.size() == nb * RT_BOXC_F4;
         // node collapse (plan_collapse): planned for the camera, so rebuilt when it or the image size changes
-        const bool use_c = c->collapse > 0 && (c->variant == 0 || c->variant == 39) && c->have_cam;
+        const bool use_c = c->collapse && (c->variant == 0 || c->variant == 39) && c->have_cam;
         const bool cam_moved = use_c && (std::memcmp(&c->walk_cam, &c->cam, sizeof(rt_camera_ubo)) != 0 ||
                                          c->walk_w != c->width || c->walk_h != c->height);
         const bool use_r = c->rebuild > 0 && (c->variant == 0 || c->variant == 39);
         if (c->walk_stale || use_v != c->walk_v || (use_v && a.box_margin != c->walk_v_margin) ||
-            use_c != c->walk_c || cam_moved || use_r != c->walk_r || c->rebuild != c->walk_rmode ||
-            c->collapse != c->walk_cmode) {
+            use_c != c->walk_c || cam_moved || use_r != c->walk_r || c->rebuild != c->walk_rmode) {
             if (c->walk_stale) c->rb_mode = -1;   // a new walk_dn (validate)
             if (use_r && c->rb_mode != c->rebuild) {
                 c->rb_dn = rebuild_inner(c->walk_dn, c->rebuild);
@@ -2103,19 +2021,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             const std::vector<rt_dnode>& rb = use_r ? c->rb_dn : none;
             const std::vector<rt_dnode>& wdn = rb.empty() ? c->walk_dn : rb;
             std::vector<uint8_t> drop;
-            PrimRecs pr;
-            if (c->collapse == 2) {
-                const std::vector<uint8_t>& SB = c->host_buf[RT_BIND_SPHERES];
-                const std::vector<uint8_t>& QB = c->host_buf[RT_BIND_QUADS];
-                const std::vector<uint8_t>& BB = c->host_buf[RT_BIND_BOXES];
-                pr.sph = (const rt_sphere*)SB.data();
-                pr.ns = SB.size() / sizeof(rt_sphere);
-                pr.quad = (const rt_quad*)QB.data();
-                pr.nq = QB.size() / sizeof(rt_quad);
-                pr.box = (const rt_box*)BB.data();
-                pr.nb = BB.size() / sizeof(rt_box);
-            }
-            if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height, c->collapse == 2 ? &pr : nullptr);
+            if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height);
             c->n_dropped = 0;
             for (uint8_t x : drop) c->n_dropped += x;
             const std::vector<uint8_t>* dp = c->n_dropped ? &drop : nullptr;
@@ -2143,7 +2049,6 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             }
             if (!use_v) c->n_vnodes = 0;
             c->walk_c = use_c;
-            c->walk_cmode = c->collapse;
             c->walk_r = use_r;
             c->walk_rmode = c->rebuild;
             c->n_rebuilt = rb.empty() ? 0 : (int)rb.size();
@@ -2852,7 +2757,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_SHADE_LDS: c->shade_lds = v != 0; break;
         case RT_OPTION_BOX_VNODES: c->box_vnodes = v != 0; break;
         case RT_OPTION_ZERO_DIR_END: c->zero_dir_end = v != 0; break;
-        case RT_OPTION_COLLAPSE: if (v < 0 || v > 2) return bad(); c->collapse = v; break;
+        case RT_OPTION_COLLAPSE: c->collapse = v != 0; break;
         case RT_OPTION_REBUILD: if (v < 0 || v > 2) return bad(); c->rebuild = v; break;
         case RT_OPTION_CHUNK_TARGET: if (v < 0) return bad(); c->chunk_target = v; break;
         case RT_OPTION_STAGED_CHUNK_TARGET: if (v < 1) return bad(); c->staged_chunk_target = v; break;
