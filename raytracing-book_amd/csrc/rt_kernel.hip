@@ -333,7 +333,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
             v3 cur3;
             h.t = tmax;   // the accepted hit's t (unused on a miss)
-            bool done = after_trace<BOXC>(P, S, h, has, fx, fy, cur3);
+            bool done = after_trace<BOXC, STATS>(P, S, h, has, fx, fy, cur3, st);
             if (!done && S.depth >= P.max_depth) {   // the loop is exhausted: final_color stays vec3(0)
                 cur3 = mk3s(0.0f);
                 done = true;

@@ -77,8 +77,13 @@ enum {
     // wave executions with 1..8 active lanes (a wave64 VALU instruction with <= 8 exec lanes
     // occupies the SIMD 1.4-5x longer than with >= 9 in a register-only loop: tools/exec_ops.hip):
     // the leaf slots' type blocks and the node steps
-    ST_SPH_SM, ST_QUAD_SM, ST_BOX_SM, ST_MED_SM, ST_NODE_SM, ST_N
+    ST_SPH_SM, ST_QUAD_SM, ST_BOX_SM, ST_MED_SM, ST_NODE_SM,
+    // shading (round 5): wave-cycles of its parts -- the hit record, the material's scatter, the
+    // mixture pdf, the texture lookups -- and the material blocks' executions and lanes
+    ST_SH_HIT_CYC, ST_SH_SCAT_CYC, ST_SH_MIX_CYC, ST_SH_TEX_CYC, ST_SH_LAM_IT, ST_SH_LAM_LN, ST_SH_ISO_IT,
+    ST_SH_ISO_LN, ST_SH_MET_IT, ST_SH_MET_LN, ST_SH_DIE_IT, ST_SH_DIE_LN, ST_N
 };
+static_assert(ST_N <= 64, "rt_debug_read_stats reads 64 counters");
 __device__ __forceinline__ bool first_active_lane() {
     unsigned long long m = __ballot(1);
     return (unsigned)__lane_id() == (unsigned)(__ffsll((long long)m) - 1);
@@ -1181,8 +1186,10 @@ struct Path {
 
 // The shading half of ray_color's loop body (compute.glsl:310-339) for a hit.
 // Returns true when the path ended, with its color in `result`.
-template <bool PK_INLINE = false>
-__device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float px, float py, v3& result) {
+template <bool PK_INLINE = false, bool STATS = false>
+__device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float px, float py, v3& result,
+                                      unsigned long long* st = nullptr) {
+    unsigned long long c0 = STATS ? clock64() : 0;
     v3 d = S.d;
     // hit_record of the closest hit: p = ray.o + ray.dir*t (hitting.glsl:39,104,188)
     v3 p = add3(S.o, scale3(d, h.t));
@@ -1247,6 +1254,15 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     // scatter (scatter.glsl:43-98)
     int mid = (material >> 16) & 0xFFFF;
     bool skip_pdf = false, should = false;
+    if (STATS) {
+        const unsigned long long c1 = clock64();
+        st_add(st, ST_SH_HIT_CYC, c1 - c0);
+        c0 = c1;
+        st_pred(st, mid == RT_MAT_LAMBERTIAN, ST_SH_LAM_IT, ST_SH_LAM_LN);
+        st_pred(st, mid == RT_MAT_ISOTROPIC, ST_SH_ISO_IT, ST_SH_ISO_LN);
+        st_pred(st, mid == RT_MAT_METAL, ST_SH_MET_IT, ST_SH_MET_LN);
+        st_pred(st, mid == RT_MAT_DIELECTRIC, ST_SH_DIE_IT, ST_SH_DIE_LN);
+    }
     if (mid == RT_MAT_DIFFUSE_LIGHT) {
         result = mul3(S.acc, emis);
         return true;
@@ -1290,6 +1306,11 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         should = true;
     }
     if ((fabsf(d.x) < 1e-8f) && (fabsf(d.y) < 1e-8f) && (fabsf(d.z) < 1e-8f)) d = normal;
+    if (STATS) {
+        const unsigned long long c1 = clock64();
+        st_add(st, ST_SH_SCAT_CYC, c1 - c0);
+        c0 = c1;
+    }
     if (!should) {
         result = mul3(S.acc, emis);
         return true;
@@ -1298,6 +1319,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     if (skip_pdf) {
         S.acc = mul3(S.acc, texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time));
         S.d = d;
+        if (STATS) st_add(st, ST_SH_TEX_CYC, clock64() - c0);
         return false;
     }
     if (rnd(rf, px, py) < 0.5f) d = lights_random(P, p, rf, px, py);
@@ -1320,7 +1342,13 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     if (mid == RT_MAT_LAMBERTIAN) spdf = g_max(0.0f, g_dot(normal, g_normalize(d)) / RT_PI);
     else if (mid == RT_MAT_ISOTROPIC) spdf = 1.0f / (4.0f * RT_PI);
     else spdf = 0.0f;
+    if (STATS) {
+        const unsigned long long c1 = clock64();
+        st_add(st, ST_SH_MIX_CYC, c1 - c0);
+        c0 = c1;
+    }
     v3 att = texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time);
+    if (STATS) st_add(st, ST_SH_TEX_CYC, clock64() - c0);
     S.acc = mul3(S.acc, divs3(scale3(att, spdf), pdf));
     S.d = d;
     return false;
@@ -1328,9 +1356,9 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 
 // The rest of ray_color's loop body after the walk (compute.glsl:308-340): the
 // uv the walk left (compute.glsl:62), the background on a miss, else shade().
-template <bool PK_INLINE = false>
+template <bool PK_INLINE = false, bool STATS = false>
 __device__ __forceinline__ bool after_trace(const KP& P, Path& S, const Hit& h, bool hit, float px, float py,
-                                            v3& result) {
+                                            v3& result, unsigned long long* st = nullptr) {
     if (h.uv_kind_idx != 0) {
         bool sph = (h.uv_kind_idx >> 16) == 1;
         v3 up = add3(S.o, scale3(S.d, h.uv_a));   // the sphere hit's p (hitting.glsl:39)
@@ -1343,7 +1371,7 @@ __device__ __forceinline__ bool after_trace(const KP& P, Path& S, const Hit& h, 
         result = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
         return true;
     }
-    return shade<PK_INLINE>(P, S, h, px, py, result);
+    return shade<PK_INLINE, STATS>(P, S, h, px, py, result, st);
 }
 
 // Camera ray of frame `frame_count` (compute.glsl:345-350, random.glsl:19-30,82-100).

@@ -15,7 +15,9 @@ NAMES = ["TOTAL", "START_CYC", "START_IT", "START_LN", "NODE_CYC", "NODE_IT", "N
          "QUAD_IT", "BOX_IT", "MED_IT", "FAST_TRACES", "FAST_EXACT"] + [f"FAST_WHY{r}" for r in range(1, 10)] + [
          "FAST_STEPS", "FAST_TESTS", "FAST_PRE_CYC", "FAST_POST_CYC", "FAST_EXACT_CYC",
          "SPH_CYC", "QUAD_CYC", "BOX_CYC", "MED_CYC", "TRACE_IT", "TRACE_LN", "ROUND_IT", "ROUND_LN",
-         "RET_IT", "RET_LN", "SPH_SM", "QUAD_SM", "BOX_SM", "MED_SM", "NODE_SM"]
+         "RET_IT", "RET_LN", "SPH_SM", "QUAD_SM", "BOX_SM", "MED_SM", "NODE_SM",
+         "SH_HIT_CYC", "SH_SCAT_CYC", "SH_MIX_CYC", "SH_TEX_CYC", "SH_LAM_IT", "SH_LAM_LN", "SH_ISO_IT", "SH_ISO_LN",
+         "SH_MET_IT", "SH_MET_LN", "SH_DIE_IT", "SH_DIE_LN"]
 
 
 def main():
@@ -64,6 +66,12 @@ def main():
         print(f"  link walk: {v['TRACE_LN'] / v['TRACE_IT']:5.2f} lanes per wave trace, "
               f"{v['ROUND_IT'] / v['TRACE_IT']:5.2f} node-walk+leaf rounds per wave trace, "
               f"{v['ROUND_LN'] / (64.0 * max(v['ROUND_IT'], 1)) * 100:5.1f}% of lanes still tracing per round")
+    if v["SH_HIT_CYC"]:
+        print("  shading parts: " + "  ".join(f"{k} {100.0 * v['SH_' + k + '_CYC'] / tot:4.1f}%" for k in ("HIT", "SCAT", "MIX", "TEX"))
+              + " of wave-cycles")
+        for m in ("LAM", "ISO", "MET", "DIE"):
+            it, ln = v[f"SH_{m}_IT"], v[f"SH_{m}_LN"]
+            print(f"  material {m}: wave-executions {it:.3e} lanes/exec {ln / max(it, 1):5.2f}  per-sample {ln / samples:5.2f}")
     if v["ROUND_IT"]:
         print(f"  rounds with retired lanes: {v['RET_IT'] / v['ROUND_IT'] * 100:5.1f}% of rounds, "
               f"{v['RET_LN'] / (64.0 * v['ROUND_IT']) * 100:5.1f}% of lane-rounds retired (unit tails)")
