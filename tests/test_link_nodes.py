@@ -442,3 +442,33 @@ def test_rebuilt_inner_nodes_test_the_same_leaves(sid, rebuild):
         assert got == want, (r, o, d)
         differ += len(want) > 0
     assert differ > 50
+
+
+@pytest.mark.parametrize("rebuild", [1, 2])
+def test_rebuilt_inner_nodes_of_a_4000_sphere_cloud(rebuild):
+    """The same replay on the ~4000-node cloud (tests/adversarial.py): about 2000 leaves, so the
+    dynamic programme runs with its Knuth window over a long sequence (rebuild=2)."""
+    import adversarial
+    scene = adversarial.sphere_cloud(4000, 4)
+    tn = threaded(scene)
+    n = len(tn)
+    ln, drop, nd = collapse_links(scene, 64, 48, rebuild=rebuild)
+    nk = n - nd
+    rng = np.random.default_rng(400 + rebuild)
+    boxes = np.stack([x["box"] for x in tn])
+    lo, hi = boxes[0, 0::2], boxes[0, 1::2]
+    cam = scene.camera[4:7].astype(np.float32)
+    hits = 0
+    for r in range(120):
+        o = cam if r % 2 == 0 else (lo + (hi - lo) * rng.random(3)).astype(np.float32)
+        d = rng.normal(size=3).astype(np.float32)
+        if r % 9 == 0:
+            d[rng.integers(3)] = 0.0
+        with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+            inv = (np.float32(1.0) / d).astype(np.float32)
+            exact = bool(np.any(inv == -np.inf))
+            want = walk_tree_rays(tn, o, d, inv, exact)
+            got = walk_links_rays(ln, nk, o, d, inv, exact)
+        assert got == want, r
+        hits += len(want) > 0
+    assert hits > 20
