@@ -1015,6 +1015,9 @@ __device__ __forceinline__ v2 resolve_uv(const KP& P, const UvSrc& s, float time
 // texture.glsl:112-132
 template <bool PK_INLINE = false>
 __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvSrc& uvs, float time) {
+#ifdef RT_AB_KNOBS
+    if (P.debug_flags & 4) return mk3s(0.5f);   // ablation only (A/B build): every texture a constant, never exact
+#endif
     int detail_i = id & 0xFFF;
     int index = (id >> 12) & 0xFFFF;
     int type = (id >> 28) & 0xF;

@@ -36,12 +36,14 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--ab", action="store_true", help="the A/B library (ablation options such as debug_flags; "
+                                                        "their images are not bit-identical by design)")
     a = ap.parse_args()
     specs = a.specs.split(",")
     scene = rtamd.Scene(a.scene, a.width, a.height, seed=1)
     ctxs = {}
     for s in specs:
-        c = rtamd.RenderContext(devices=(0,), options=parse(s))
+        c = rtamd.RenderContext(devices=(0,), options=parse(s), ab=a.ab)
         c.upload_scene(scene)
         c.set_params(max_depth=a.depth, spp=4096)
         c.resize(a.width, a.height)
