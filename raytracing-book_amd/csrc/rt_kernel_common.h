@@ -857,6 +857,37 @@ __device__ __forceinline__ void texel_slot(const KP& P, int slot, int x, int y, 
     }
     texel(P.tex[slot], x, y, out);
 }
+// texel_slot of row 0 at x0, x0 + 1 and x0 + 2 (a checker's colours and scale): one descriptor read,
+// then the three texel reads at once -- the same values as three texel_slot calls
+__device__ __forceinline__ void texels3_slot(const KP& P, int slot, int x0, float a[3], float b[3], float c[3]) {
+    if (P.tex_lds >= 0) {
+        const float4 dsc = rt_dyn_lds[P.tex_lds + slot];
+        const int w = __float_as_int(dsc.x), h = __float_as_int(dsc.y), off = __float_as_int(dsc.w);
+        if (off >= 0) {
+            const uint32_t* tex = reinterpret_cast<const uint32_t*>(rt_dyn_lds + off);
+            float* outs[3] = {a, b, c};
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const int x = x0 + k;
+                float* out = outs[k];
+                out[0] = out[1] = out[2] = 0.0f;
+                if (x < 0 || x >= w || h <= 0) continue;
+                const uint32_t v = tex[x];
+                if (__float_as_int(dsc.z)) {
+                    out[0] = __uint_as_float(v);
+                } else {
+                    out[0] = unorm8_fast(v & 0xFFu);
+                    out[1] = unorm8_fast((v >> 8) & 0xFFu);
+                    out[2] = unorm8_fast((v >> 16) & 0xFFu);
+                }
+            }
+            return;
+        }
+    }
+    texel(P.tex[slot], x0, 0, a);
+    texel(P.tex[slot], x0 + 1, 0, b);
+    texel(P.tex[slot], x0 + 2, 0, c);
+}
 __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
     float t[3];
     texel(T, x, y, t);
@@ -1028,14 +1059,16 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_CHECKER) {   // :6-17
+        // the scale (texel pix + 2) and both colours read at once: the colour's choice does not
+        // change the texels, only which one is returned
         int pix = detail_i * 3;
-        texel_slot(P, index & 7, pix + 2, 0, t);
+        float even[3], odd[3];
+        texels3_slot(P, index & 7, pix, even, odd, t);
         float scale = t[0];
         float inv_scale = 1.0f / scale;
         v3 q = scale3(p, inv_scale);
         int s = rt_f2i(q.x) + rt_f2i(q.y) + rt_f2i(q.z);
-        texel_slot(P, index & 7, (s % 2 == 0) ? pix : pix + 1, 0, t);
-        return mk3(t[0], t[1], t[2]);
+        return (s % 2 == 0) ? mk3(even[0], even[1], even[2]) : mk3(odd[0], odd[1], odd[2]);
     }
     if (type == RT_TEXTYPE_PERLIN) {    // :79-94
 #ifdef RT_AB_KNOBS
