@@ -857,37 +857,6 @@ __device__ __forceinline__ void texel_slot(const KP& P, int slot, int x, int y, 
     }
     texel(P.tex[slot], x, y, out);
 }
-// texel_slot of row 0 at x0, x0 + 1 and x0 + 2 (a checker's colours and scale): one descriptor read,
-// then the three texel reads at once -- the same values as three texel_slot calls
-__device__ __forceinline__ void texels3_slot(const KP& P, int slot, int x0, float a[3], float b[3], float c[3]) {
-    if (P.tex_lds >= 0) {
-        const float4 dsc = rt_dyn_lds[P.tex_lds + slot];
-        const int w = __float_as_int(dsc.x), h = __float_as_int(dsc.y), off = __float_as_int(dsc.w);
-        if (off >= 0) {
-            const uint32_t* tex = reinterpret_cast<const uint32_t*>(rt_dyn_lds + off);
-            float* outs[3] = {a, b, c};
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                const int x = x0 + k;
-                float* out = outs[k];
-                out[0] = out[1] = out[2] = 0.0f;
-                if (x < 0 || x >= w || h <= 0) continue;
-                const uint32_t v = tex[x];
-                if (__float_as_int(dsc.z)) {
-                    out[0] = __uint_as_float(v);
-                } else {
-                    out[0] = unorm8_fast(v & 0xFFu);
-                    out[1] = unorm8_fast((v >> 8) & 0xFFu);
-                    out[2] = unorm8_fast((v >> 16) & 0xFFu);
-                }
-            }
-            return;
-        }
-    }
-    texel(P.tex[slot], x0, 0, a);
-    texel(P.tex[slot], x0 + 1, 0, b);
-    texel(P.tex[slot], x0 + 2, 0, c);
-}
 __device__ __forceinline__ float texel_r(const rt_dtex& T, int x, int y) {
     float t[3];
     texel(T, x, y, t);
@@ -1059,16 +1028,14 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_CHECKER) {   // :6-17
-        // the scale (texel pix + 2) and both colours read at once: the colour's choice does not
-        // change the texels, only which one is returned
         int pix = detail_i * 3;
-        float even[3], odd[3];
-        texels3_slot(P, index & 7, pix, even, odd, t);
+        texel_slot(P, index & 7, pix + 2, 0, t);
         float scale = t[0];
         float inv_scale = 1.0f / scale;
         v3 q = scale3(p, inv_scale);
         int s = rt_f2i(q.x) + rt_f2i(q.y) + rt_f2i(q.z);
-        return (s % 2 == 0) ? mk3(even[0], even[1], even[2]) : mk3(odd[0], odd[1], odd[2]);
+        texel_slot(P, index & 7, (s % 2 == 0) ? pix : pix + 1, 0, t);
+        return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_PERLIN) {    // :79-94
 #ifdef RT_AB_KNOBS
@@ -1256,8 +1223,13 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     } else if (h_type == RT_MODEL_CONSTANT_MEDIUM) {   // hitting.glsl:189-190 + compute.glsl:211-216
         normal = mk3(1.0f, 0.0f, 0.0f);
         front = true;
-        material = ldg_i(&P.media[h_idx].phase_material);
-        tex_id = ldg_i(&P.media[h_idx].texture_id);
+        if (P.media_lds >= 0) {   // the medium's LDS record: phase material in R0.w, texture id in R1.w
+            material = __float_as_int(rt_dyn_lds[P.media_lds + 3 * h_idx].w);
+            tex_id = __float_as_int(rt_dyn_lds[P.media_lds + 3 * h_idx + 1].w);
+        } else {
+            material = ldg_i(&P.media[h_idx].phase_material);
+            tex_id = ldg_i(&P.media[h_idx].texture_id);
+        }
     } else if (h_type == RT_MODEL_BOX && P.box_mat_lds >= 0) {
         // a compact box from the shading tables: face h_face's normal rebuilt bit for bit from the
         // compact record (canonical axis and value, the zero components' signs in c2.w), material,
@@ -1501,6 +1473,8 @@ __device__ __forceinline__ void stage_lds(const KP& P, float4* s_nodes, int tid)
     if (P.perlin_lds >= 0)   // the packed Perlin table after the nodes (host-sized launch)
         for (int k = tid; k < 256; k += BLOCK) s_nodes[P.perlin_lds + k] = ldg(P.perlin_pk + k);
     if (P.media_lds >= 0) {   // per medium: (boundary idx, type, -1/density, phase), sphere A, B
+        // (R1.w, the boundary sphere's texture id, which the boundary test does not read, holds the
+        // medium's texture id for the shading)
         for (int k = tid; k < 3 * P.n_media; k += BLOCK) {
             const rt_medium& m = P.media[k / 3];
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1509,6 +1483,7 @@ __device__ __forceinline__ void stage_lds(const KP& P, float4* s_nodes, int tid)
                                 __int_as_float(m.phase_material));
             else if (m.boundary_type == RT_MODEL_SPHERE)
                 v = reinterpret_cast<const float4*>(P.spheres + m.boundary_idx)[k % 3 - 1];
+            if (k % 3 == 1) v.w = __int_as_float(m.texture_id);
             s_nodes[P.media_lds + k] = v;
         }
     }
