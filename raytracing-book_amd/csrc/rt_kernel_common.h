@@ -1223,13 +1223,8 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     } else if (h_type == RT_MODEL_CONSTANT_MEDIUM) {   // hitting.glsl:189-190 + compute.glsl:211-216
         normal = mk3(1.0f, 0.0f, 0.0f);
         front = true;
-        if (P.media_lds >= 0) {   // the medium's LDS record: phase material in R0.w, texture id in R1.w
-            material = __float_as_int(rt_dyn_lds[P.media_lds + 3 * h_idx].w);
-            tex_id = __float_as_int(rt_dyn_lds[P.media_lds + 3 * h_idx + 1].w);
-        } else {
-            material = ldg_i(&P.media[h_idx].phase_material);
-            tex_id = ldg_i(&P.media[h_idx].texture_id);
-        }
+        material = ldg_i(&P.media[h_idx].phase_material);
+        tex_id = ldg_i(&P.media[h_idx].texture_id);
     } else if (h_type == RT_MODEL_BOX && P.box_mat_lds >= 0) {
         // a compact box from the shading tables: face h_face's normal rebuilt bit for bit from the
         // compact record (canonical axis and value, the zero components' signs in c2.w), material,
@@ -1473,8 +1468,6 @@ __device__ __forceinline__ void stage_lds(const KP& P, float4* s_nodes, int tid)
     if (P.perlin_lds >= 0)   // the packed Perlin table after the nodes (host-sized launch)
         for (int k = tid; k < 256; k += BLOCK) s_nodes[P.perlin_lds + k] = ldg(P.perlin_pk + k);
     if (P.media_lds >= 0) {   // per medium: (boundary idx, type, -1/density, phase), sphere A, B
-        // (R1.w, the boundary sphere's texture id, which the boundary test does not read, holds the
-        // medium's texture id for the shading)
         for (int k = tid; k < 3 * P.n_media; k += BLOCK) {
             const rt_medium& m = P.media[k / 3];
             float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1483,7 +1476,6 @@ __device__ __forceinline__ void stage_lds(const KP& P, float4* s_nodes, int tid)
                                 __int_as_float(m.phase_material));
             else if (m.boundary_type == RT_MODEL_SPHERE)
                 v = reinterpret_cast<const float4*>(P.spheres + m.boundary_idx)[k % 3 - 1];
-            if (k % 3 == 1) v.w = __int_as_float(m.texture_id);
             s_nodes[P.media_lds + k] = v;
         }
     }
