@@ -1254,6 +1254,11 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         tex_id = __float_as_int(ldg(q0 + 2).w);
         if (front) emis = f3(ldg(q0 + 4));
     }
+    // A solid texture's colour (texture_color's first case) read here, before the scatter, so that its
+    // two dependent LDS reads overlap the scatter's arithmetic; the same texel, so the same value
+    const bool solid_tex = ((tex_id >> 28) & 0xF) == RT_TEXTYPE_SOLID;
+    float sc[3] = {0.0f, 0.0f, 0.0f};
+    if (solid_tex) texel_slot(P, (tex_id >> 12) & 7, tex_id & 0xFFF, 0, sc);
     // scatter (scatter.glsl:43-98)
     int mid = (material >> 16) & 0xFFFF;
     bool skip_pdf = false, should = false;
@@ -1320,7 +1325,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     }
     S.o = p;
     if (skip_pdf) {
-        S.acc = mul3(S.acc, texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time));
+        S.acc = mul3(S.acc, solid_tex ? mk3(sc[0], sc[1], sc[2]) : texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time));
         S.d = d;
         if (STATS) st_add(st, ST_SH_TEX_CYC, clock64() - c0);
         return false;
@@ -1350,7 +1355,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         st_add(st, ST_SH_MIX_CYC, c1 - c0);
         c0 = c1;
     }
-    v3 att = texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time);
+    v3 att = solid_tex ? mk3(sc[0], sc[1], sc[2]) : texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time);
     if (STATS) st_add(st, ST_SH_TEX_CYC, clock64() - c0);
     S.acc = mul3(S.acc, divs3(scale3(att, spdf), pdf));
     S.d = d;
