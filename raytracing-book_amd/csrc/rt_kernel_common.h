@@ -1255,8 +1255,10 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         if (front) emis = f3(ldg(q0 + 4));
     }
     // A solid texture's colour (texture_color's first case) read here, before the scatter, so that its
-    // two dependent LDS reads overlap the scatter's arithmetic; the same texel, so the same value
-    const bool solid_tex = ((tex_id >> 28) & 0xF) == RT_TEXTYPE_SOLID;
+    // two dependent LDS reads overlap the scatter's arithmetic; the same texel, so the same value.
+    // Not in the compact-box kernels (PK_INLINE, scene 8): there +0.5%, scene 6 -1.5%, scene 0 -0.7%
+    // (profiles/r05_u_lib_ab.log).
+    const bool solid_tex = !PK_INLINE && ((tex_id >> 28) & 0xF) == RT_TEXTYPE_SOLID;
     float sc[3] = {0.0f, 0.0f, 0.0f};
     if (solid_tex) texel_slot(P, (tex_id >> 12) & 7, tex_id & 0xFFF, 0, sc);
     // scatter (scatter.glsl:43-98)
