@@ -959,7 +959,7 @@ __device__ __forceinline__ float perlin_turb_lds_in(int at, float px, float py, 
     const float4* tab = rt_dyn_lds + at;
     float accum = 0.0f, weight = 1.0f;
     v3 q = mk3(px, py, pz);
-#pragma unroll 2
+#pragma unroll 1
     for (int o = 0; o < 7; o++) {
         accum += weight * perlin_noise_pk(tab, q);
         weight *= 0.5f;
