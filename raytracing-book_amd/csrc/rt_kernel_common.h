@@ -49,6 +49,15 @@ __device__ __forceinline__ float4 ldg(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ int ldg_i(const int* p) { return *(__attribute__((address_space(1))) const int*)p; }
+// The same loads through the constant address space: with a uniform address (a record every lane
+// reads, e.g. the lights' in lights_pdf_value) the compiler issues a scalar load (s_load, the
+// scalar cache, no vector registers); with a divergent one an ordinary vector load.
+typedef __attribute__((address_space(4))) const f4v c_f4v;
+__device__ __forceinline__ float4 ldc(const float4* p) {
+    const f4v v = *(const c_f4v*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int ldc_i(const int* p) { return *(__attribute__((address_space(4))) const int*)p; }
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint2 ldg_u2(const uint2* p) {
     const u2v v = *(__attribute__((address_space(1))) const u2v*)p;
@@ -241,8 +250,8 @@ __device__ __forceinline__ bool face_interior(float4 A, float4 B, v3 o, v3 d, fl
 // Q0, Q1 = the record's first two float4 (loaded by the caller).
 __device__ __forceinline__ bool quad_test_ab(const float4* __restrict__ f, float4 Q0, float4 Q1, v3 o, v3 d,
                                              float tmin, float tmax, float& t, float& alpha, float& beta,
-                                             bool fd = false) {
-    const float4 Q2 = ldg(f + 2);
+                                             bool fd = false, bool uniform = false) {
+    const float4 Q2 = uniform ? ldc(f + 2) : ldg(f + 2);
     v3 n = f3(Q0);
     float denom = g_dot(n, d);
     if (fabsf(denom) < 1e-8f) return false;
@@ -1104,11 +1113,12 @@ __device__ __forceinline__ v3 rand_unit_vec(float& rf, float px, float py) {
 }
 
 // pdf.glsl:11-24
+// idx is the same in every lane (lights_pdf_value's loop): the records by scalar loads (ldc)
 __device__ __forceinline__ float sphere_light_pdf(const KP& P, int idx, v3 o, v3 d, float time) {
     const float4* sp = reinterpret_cast<const float4*>(P.spheres + idx);
+    const float4 A = ldc(sp), B = ldc(sp + 1);
     float t;
-    if (!sphere_t(sp, time, o, d, g_dot(d, d), 0.001f, RT_INFINITY, t)) return 0.0f;
-    float4 A = ldg(sp), B = ldg(sp + 1);
+    if (!sphere_t_ab(A, B, time, o, d, g_dot(d, d), 0.001f, RT_INFINITY, t)) return 0.0f;
     v3 pc = sub3(f3(A), o);
     float d2 = g_dot(pc, pc);
     float ctm = sqrtf(1.0f - B.w * B.w / d2);
@@ -1119,14 +1129,15 @@ __device__ __forceinline__ float sphere_light_pdf(const KP& P, int idx, v3 o, v3
 // pdf.glsl:41-51
 __device__ __forceinline__ float quad_light_pdf(const KP& P, int idx, v3 o, v3 d) {
     const float4* q = reinterpret_cast<const float4*>(P.quads + idx);
+    const float4* f = P.dquads + RT_DFACE_F4 * idx;
     float t, al, be;
-    if (!quad_test(P.dquads + RT_DFACE_F4 * idx, o, d, 0.001f, RT_INFINITY, t, al, be)) return 0.0f;
-    v3 n = f3(ldg(q));
+    if (!quad_test_ab(f, ldc(f), ldc(f + 1), o, d, 0.001f, RT_INFINITY, t, al, be, false, true)) return 0.0f;
+    v3 n = f3(ldc(q));
     bool front = g_dot(d, n) < 0.0f;
     v3 normal = front ? n : neg3(n);
     float d2 = t * t * g_dot(d, d);
     float cosine = fabsf(g_dot(d, normal) / g_length(d));
-    return d2 / (cosine * ldg(q + 3).w);
+    return d2 / (cosine * ldc(q + 3).w);
 }
 
 // pdf.glsl:58-81
@@ -1134,7 +1145,7 @@ __device__ __forceinline__ float lights_pdf_value(const KP& P, v3 o, v3 d, float
     float weight = 1.0f / (float)P.lights_count;
     float sum = 0.0f;
     for (int i = 0; i < P.lights_count; i++) {
-        int packed = ldg_i(P.lights + i);
+        int packed = ldc_i(P.lights + i);   // the same in every lane: a scalar load
         int type = (packed >> 16) & 0xFFFF, idx = packed & 0xFFFF;
         float pdf = 0.0f;
         if (type == RT_MODEL_SPHERE) pdf = sphere_light_pdf(P, idx, o, d, time);
