@@ -37,6 +37,7 @@ import json
 import math
 import os
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -80,6 +81,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=60.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--png", default=None)
+    p.add_argument("--comm-timeout-ms", type=int, default=60000,
+                   help="deadline of the native RCCL gather's rt_comm_init / rt_gather_image (rt_comm_set_timeout)")
+    p.add_argument("--gather-deadline", type=float, default=240.0,
+                   help="N > 1: seconds after the timed region by which gather + parity check must finish, "
+                        "else the line is printed with the timed value and gather_path 'timeout' (LineGuard)")
     p.add_argument("--fast-bvh", action="store_true",
                    help="the non-parity fast mode (rt_set_bvh_mode RT_BVH_SAH): a separate line, never the headline")
     a = p.parse_args()
@@ -356,6 +362,61 @@ def roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms):
     return out
 
 
+# ---------------------------------------------------------------- the line survives the gather
+class LineGuard:
+    """the timed value cannot be lost to the exchange after the timed region.
+
+    Everything the line needs from the timed region is in `out` before the gather starts.  A
+    watchdog (a daemon timer, `deadline_s`) then bounds the gather, its torch fallback and the
+    gather parity check together: if they have not finished by then, rank 0 prints the line
+    with the timed value and gather_path "timeout", every rank logs it and leaves with status 0
+    (`exit_fn`, os._exit: a process blocked inside RCCL or a collective cannot unwind).  The
+    product path is bounded itself as well (rt_comm_set_timeout, native_gather's timeout_ms);
+    this is the last line of defence.  Exactly one line is printed either way."""
+
+    def __init__(self, out, rank, deadline_s, exit_fn=os._exit, stream=None):
+        self.out, self.rank, self.deadline_s, self.exit_fn = out, rank, deadline_s, exit_fn
+        self.stream = stream
+        self.lock = threading.Lock()
+        self.printed = False
+        self.timer = None
+        if deadline_s and deadline_s > 0:
+            self.timer = threading.Timer(deadline_s, self._fire)
+            self.timer.daemon = True
+            self.timer.start()
+
+    def _print(self, line):
+        print(json.dumps(line), file=self.stream or sys.stdout, flush=True)
+
+    def _fire(self):
+        with self.lock:
+            if not self.printed and self.rank == 0:
+                line = dict(self.out)
+                line.update(gather_path="timeout", gather_native_error=(
+                    f"gather + parity check did not finish within {self.deadline_s:g} s of the timed region; "
+                    "the timed value stands"), gather_parity=None)
+                self._print(line)
+            self.printed = True
+        log(f"rank {self.rank}: gather watchdog fired after {self.deadline_s:g} s; leaving")
+        self.exit_fn(0)
+
+    def emit(self, extra):
+        """Print the line (rank 0) with the post-gather fields, unless the watchdog already did.
+        The watchdog keeps running until close(): the final barrier is bounded too."""
+        with self.lock:
+            if self.printed:
+                return
+            self.printed = True
+            if self.rank == 0:
+                line = dict(self.out)
+                line.update(extra)
+                self._print(line)
+
+    def close(self):
+        if self.timer:
+            self.timer.cancel()
+
+
 def main():
     args = parse()
     import torch
@@ -433,73 +494,11 @@ def main():
 
     samples_total = args.width * args.height * F * args.steps   # all ranks together
     value = samples_total / t_max / 1e6
-
-    # Gather of the accumulated stripes to rank 0 (reported separately, not in value): the
-    # product's path behind the C ABI first (rt_comm_init + rt_gather_image: ncclSend to rank 0,
-    # de-interleave kernel there; what a Java host calls), torch.distributed.gather as the
-    # reported fallback if that path fails (e.g. several ranks on one GPU in a rehearsal).
-    full, gather_path, gather_err = None, None, None
-    torch.cuda.synchronize()
-    tg = time.perf_counter()
-    try:
-        if os.environ.get("RT_BENCH_GATHER") == "torch":   # escape hatch: the torch gather only
-            raise RuntimeError("RT_BENCH_GATHER=torch")
-        full = rdist.native_gather(ctx, rank, world)
-        gather_path = "rt_gather_image (RCCL send/recv + device de-interleave)" if world > 1 \
-            else "rt_read_image (world 1)"
-    except Exception as e:   # noqa: BLE001 -- any failure of the native path falls back
-        gather_err = repr(e)[:300]
-        log("native gather failed, falling back to torch.distributed.gather:", gather_err)
-    ok = torch.tensor([0.0 if full is None and (rank == 0 or gather_err) else 1.0], dtype=torch.float64)
-    if world > 1:   # every rank takes the same path
-        ok = ok.to(f"cuda:{dev}" if torch.distributed.get_backend() == "nccl" else "cpu")
-        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
-    if float(ok.item()) < 1.0:
-        full = rdist.gather_image(image, args.height, world, args.stripe_rows)
-        gather_path = "torch.distributed.gather (fallback)"
-    torch.cuda.synchronize()
-    gather_ms = (time.perf_counter() - tg) * 1e3
-
-    if rank != 0:
-        if world > 1:
-            torch.distributed.barrier()
-            torch.distributed.destroy_process_group()
-        return
-
-    if args.png:
-        rtamd.save_png(full, args.png)
-    nan_px = int(np.isnan(full[..., :3]).any(axis=-1).sum())
-    g_ok, g_stripes = None, []
-    if world > 1 and not args.fast_bvh:   # other ranks wait in the final barrier meanwhile
-        try:
-            g_ok, g_stripes = gather_parity(scene, args, full, world, dev, factors, F * total_steps)
-        except Exception as e:  # noqa: BLE001 -- reported, never fatal
-            log("gather parity check failed to run:", repr(e))
-
-    cpu = None
-    # the CPU baseline is an N = 1 figure (rank 0 of a one-GPU run); an N-rank run skips it so
-    # the other ranks do not idle in the final barrier for a minute
-    if not args.no_cpu_baseline and world == 1:
-        try:
-            cpu = cpu_baseline(scene, args)
-        except Exception as e:  # the baseline is reported, not required
-            log("cpu baseline failed:", repr(e))
-
     frames_per_launch = math.ceil(F / launches_per_step)
     samples_per_launch = n_local_px * frames_per_launch
-    roof = roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms)
 
-    fast = None
-    if args.fast_bvh:
-        fast = {"mode": "RT_BVH_SAH (rt_set_bvh_mode): non-parity fast mode, NOT the headline",
-                "parity": "statistical against the reference BVH (tests/test_gpu_fast_bvh.py, the gallery anchors); "
-                          "bit-exact against the oracle walking the same SAH tree",
-                "bvh_mode_ran": ctx.last_launch()["bvh_mode"]}
-        try:
-            fast["bvh_counts"] = bvh_counts(scene, args)
-        except Exception as e:  # noqa: BLE001 -- reported
-            fast["bvh_counts_error"] = repr(e)
-
+    # The line's timed fields, complete before anything else runs (LineGuard): the gather below
+    # cannot lose them.
     out = {
         "metric": METRIC + (" [fast mode: SAH BVH, non-parity]" if args.fast_bvh else ""),
         "value": round(value, 2),
@@ -519,21 +518,92 @@ def main():
                    "spp_total": args.spp_total, "spp_per_step": F, "max_depth": args.depth,
                    "stripe_rows": args.stripe_rows, "parallelism": f"row-stripes x{world}"},
         "kernel_ms_per_launch": {"max": round(max(rank_ms), 3), "min": round(min(rank_ms), 3)},
-        "gather_ms": round(gather_ms, 3),
-        "gather_path": gather_path,
-        "gather_native_error": gather_err,
-        "gather_parity": g_ok,
-        "gather_parity_stripes": len(g_stripes),
-        "nan_pixels": nan_px,
-        "roofline": roof,
-        "cpu_baseline": cpu,
+        "roofline": roofline(args, frames_per_launch, samples_per_launch, avg_launch_ms) if rank == 0 else None,
+        "cpu_baseline": None,
     }
-    if fast:
-        out["fast_bvh"] = fast
-    print(json.dumps(out), flush=True)
+    if args.fast_bvh:
+        out["fast_bvh"] = {"mode": "RT_BVH_SAH (rt_set_bvh_mode): non-parity fast mode, NOT the headline",
+                           "parity": "statistical against the reference BVH (tests/test_gpu_fast_bvh.py, the gallery "
+                                     "anchors); bit-exact against the oracle walking the same SAH tree",
+                           "bvh_mode_ran": ctx.last_launch()["bvh_mode"]}
+    if world > 1:
+        log(f"rank {rank}: timed region done, {value:.1f} Msamples/s; gathering")
+    guard = LineGuard(out, rank, args.gather_deadline if world > 1 else 0)
+    extra = finish(args, scene, ctx, image, rank, world, dev, factors, F * total_steps)
+    if rank != 0:
+        guard.emit({})
+        if world > 1:
+            torch.distributed.barrier()
+            torch.distributed.destroy_process_group()
+        guard.close()
+        return
+    if args.fast_bvh:
+        try:
+            out["fast_bvh"]["bvh_counts"] = bvh_counts(scene, args)
+        except Exception as e:  # noqa: BLE001 -- reported
+            out["fast_bvh"]["bvh_counts_error"] = repr(e)
+    cpu = None
+    # the CPU baseline is an N = 1 figure (rank 0 of a one-GPU run); an N-rank run skips it so
+    # the other ranks do not idle in the final barrier for a minute
+    if not args.no_cpu_baseline and world == 1:
+        try:
+            cpu = cpu_baseline(scene, args)
+        except Exception as e:  # the baseline is reported, not required
+            log("cpu baseline failed:", repr(e))
+    extra["cpu_baseline"] = cpu
+    guard.emit(extra)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+    guard.close()
+
+
+def finish(args, scene, ctx, image, rank, world, dev, factors, n_frames):
+    """After the timed region: the gather of the accumulated stripes to rank 0 (reported
+    separately, not in value) and, on rank 0, its bit-exact check.  The product's path behind
+    the C ABI first (rt_comm_init + rt_gather_image: ncclSend to rank 0, de-interleave kernel
+    there; what a Java host calls), bounded by --comm-timeout-ms on every rank; the torch
+    gather is the reported fallback if that path fails on any rank (e.g. several ranks on one
+    GPU in a rehearsal, or a timeout).  Returns the line's post-gather fields."""
+    import torch
+    from rtamd import dist as rdist
+    full, gather_path, gather_err = None, None, None
+    if torch.cuda.is_initialized():   # (a CPU test drives this with stand-in contexts)
+        torch.cuda.synchronize()
+    tg = time.perf_counter()
+    try:
+        if os.environ.get("RT_BENCH_GATHER") == "torch":   # escape hatch: the torch gather only
+            raise RuntimeError("RT_BENCH_GATHER=torch")
+        full = rdist.native_gather(ctx, rank, world, timeout_ms=args.comm_timeout_ms)
+        gather_path = "rt_gather_image (RCCL send/recv + device de-interleave)" if world > 1 \
+            else "rt_read_image (world 1)"
+    except Exception as e:   # noqa: BLE001 -- any failure of the native path falls back
+        gather_err = repr(e)[:300]
+        log("native gather failed, falling back to torch.distributed.gather:", gather_err)
+    ok = torch.tensor([0.0 if full is None and (rank == 0 or gather_err) else 1.0], dtype=torch.float64)
+    if world > 1:   # every rank takes the same path
+        ok = ok.to(f"cuda:{dev}" if torch.distributed.get_backend() == "nccl" else "cpu")
+        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+    if float(ok.item()) < 1.0:
+        full = rdist.gather_image(image, args.height, world, args.stripe_rows)
+        gather_path = "torch.distributed.gather (fallback)"
+    if torch.cuda.is_initialized():   # (a CPU test drives this with stand-in contexts)
+        torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    if rank != 0:
+        return {}
+    if args.png:
+        import rtamd
+        rtamd.save_png(full, args.png)
+    nan_px = int(np.isnan(full[..., :3]).any(axis=-1).sum())
+    g_ok, g_stripes = None, []
+    if world > 1 and not args.fast_bvh:   # other ranks wait in the final barrier meanwhile
+        try:
+            g_ok, g_stripes = gather_parity(scene, args, full, world, dev, factors, n_frames)
+        except Exception as e:  # noqa: BLE001 -- reported, never fatal
+            log("gather parity check failed to run:", repr(e))
+    return {"gather_ms": round(gather_ms, 3), "gather_path": gather_path, "gather_native_error": gather_err,
+            "gather_parity": g_ok, "gather_parity_stripes": len(g_stripes), "nan_pixels": nan_px}
 
 
 if __name__ == "__main__":

@@ -28,7 +28,9 @@ enum {
     RT_ERR_DEVICE = -2,       /* HIP runtime failure                               */
     RT_ERR_STATE = -3,        /* call order (e.g. render before resize)            */
     RT_ERR_LIMIT = -4,        /* an implicit reference limit exceeded (SURVEY App.C)*/
-    RT_ERR_NOMEM = -5
+    RT_ERR_NOMEM = -5,
+    RT_ERR_TIMEOUT = -6       /* rt_comm_init / rt_gather_image: a peer did not complete in
+                                 time (rt_comm_set_timeout); the communicator was aborted   */
 };
 
 /* SSBO binding points (compute.glsl:127-153, RaytraceModel.java:81-113) */
@@ -146,6 +148,15 @@ enum { RT_GATHER_HOST = 0, RT_GATHER_PEER = 1, RT_GATHER_RCCL = 2 };
 int rt_comm_unique_id(void* id_out);
 int rt_comm_init(rt_ctx* ctx, const void* id, int rank, int world);
 int rt_gather_image(rt_ctx* ctx, float* rgba);
+/* Deadline of rt_comm_init and rt_gather_image on this context, in ms (default 120000;
+ * 0 = wait forever).  The communicator is made non-blocking (ncclConfig_t.blocking = 0)
+ * where the library allows it, and every wait polls against the deadline: a rank that
+ * never joins or never posts its Send / Recv makes the call return RT_ERR_TIMEOUT, with
+ * the communicator aborted (its queued work freed), instead of holding the host. */
+int rt_comm_set_timeout(rt_ctx* ctx, int timeout_ms);
+/* Abort the context's communicator(s) (ncclCommAbort; ncclCommDestroy where absent) and
+ * free their queued work.  A later gather needs rt_comm_init again. */
+int rt_comm_abort(rt_ctx* ctx);
 /* How the last gather ran: RT_GATHER_*, or -1 before any. */
 int rt_gather_path(rt_ctx* ctx);
 

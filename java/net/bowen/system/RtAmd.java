@@ -88,6 +88,9 @@ public final class RtAmd implements AutoCloseable {
             fn("rt_comm_init", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, JAVA_INT));
     private static final MethodHandle GATHER_IMAGE = fn("rt_gather_image", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
     private static final MethodHandle GATHER_PATH = fn("rt_gather_path", FunctionDescriptor.of(JAVA_INT, ADDRESS));
+    private static final MethodHandle COMM_SET_TIMEOUT =
+            fn("rt_comm_set_timeout", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT));
+    private static final MethodHandle COMM_ABORT = fn("rt_comm_abort", FunctionDescriptor.of(JAVA_INT, ADDRESS));
 
     private final MemorySegment ctx;
     private int width, height;
@@ -172,7 +175,6 @@ public final class RtAmd implements AutoCloseable {
         }
     }
 
-    /** One process per GPU: this process renders the stripes s with s % world == rank. */
     /** rt_set_bvh_mode: RT_BVH_REFERENCE (0, the default, bit-exact) or RT_BVH_SAH (1, the non-parity
      *  fast mode: a binned-SAH tree over the same prims; statistically equal images, not bit-exact). */
     public static final int BVH_REFERENCE = 0, BVH_SAH = 1;
@@ -181,6 +183,7 @@ public final class RtAmd implements AutoCloseable {
         check(call(() -> (int) SET_BVH_MODE.invokeExact(ctx, mode)), ctx);
     }
 
+    /** One process per GPU: this process renders the stripes s with s % world == rank. */
     public void setPartition(int rank, int world, int stripeRows) {
         check(call(() -> (int) SET_PARTITION.invokeExact(ctx, rank, world, stripeRows)), ctx);
         this.rank = rank;
@@ -270,6 +273,17 @@ public final class RtAmd implements AutoCloseable {
             check(call(() -> (int) GATHER_IMAGE.invokeExact(ctx, rgba)), ctx);
             return rgba.toArray(JAVA_FLOAT);
         }
+    }
+
+    /** Deadline of commInit / gatherImage in ms (0 = none; default 120000): past it they throw with
+     *  RT_ERR_TIMEOUT (-6) and the communicator aborted, instead of waiting on a peer forever. */
+    public void commSetTimeout(int timeoutMs) {
+        check(call(() -> (int) COMM_SET_TIMEOUT.invokeExact(ctx, timeoutMs)), ctx);
+    }
+
+    /** Aborts the communicator and frees its queued work; the next gather needs commInit. */
+    public void commAbort() {
+        check(call(() -> (int) COMM_ABORT.invokeExact(ctx)), ctx);
     }
 
     /** How the last gather ran: 0 host, 1 peer copies, 2 RCCL; -1 before any. */

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -17,6 +18,7 @@
 #include <functional>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <dlfcn.h>
@@ -45,6 +47,10 @@ struct Rccl {
     decltype(&ncclGroupStart) GroupStart = nullptr;
     decltype(&ncclGroupEnd) GroupEnd = nullptr;
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
+    // optional: a non-blocking communicator (rt_comm_init), so that no RCCL call can hold the
+    // host past the context's deadline (rt_comm_set_timeout)
+    decltype(&ncclCommInitRankConfig) CommInitRankConfig = nullptr;
+    decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
 };
 Rccl& rccl() {
     static Rccl r;
@@ -56,6 +62,7 @@ Rccl& rccl() {
 #define RT_SYM(F) r.F = reinterpret_cast<decltype(r.F)>(dlsym(r.h, "nccl" #F))
             RT_SYM(GetUniqueId); RT_SYM(CommInitRank); RT_SYM(CommInitAll); RT_SYM(CommDestroy); RT_SYM(Send);
             RT_SYM(Recv); RT_SYM(GroupStart); RT_SYM(GroupEnd); RT_SYM(GetErrorString); RT_SYM(CommAbort);
+            RT_SYM(CommInitRankConfig); RT_SYM(CommGetAsyncError);
 #undef RT_SYM
             r.ok = r.GetUniqueId && r.CommInitRank && r.CommInitAll && r.CommDestroy && r.Send && r.Recv &&
                    r.GroupStart && r.GroupEnd && r.GetErrorString;
@@ -228,6 +235,8 @@ struct rt_ctx {
     int gather_path = -1;
     bool comm_tried = false;     // ncclCommInitAll of a multi-device context attempted
     bool proc_comm = false;      // rt_comm_init: one rank of a multi-process communicator
+    bool comm_nonblocking = false;   // ... made non-blocking (ncclConfig_t.blocking = 0)
+    int comm_timeout_ms = 120000;    // rt_comm_set_timeout: deadline of rt_comm_init / rt_gather_image (0: none)
 };
 
 namespace {
@@ -526,12 +535,28 @@ std::vector<float4> build_links(const std::vector<rt_dnode>& dn, const std::vect
 // exact join (min / max) of its leaves' boxes.  The reference's builder splits at the median along
 // a random axis (BVHNode.java:13-56); over scene 8's leaf order this tree takes a camera ray
 // through 35% fewer node tests (tools/node_collapse_study.py).  Leaves and their records are
-// unchanged.  Empty when a leaf box is flat or inverted (plan_collapse's condition) or the
-// tree has fewer than 3 leaves.
+// unchanged.  Empty when the uploaded tree's boxes do not nest (the reference's walk
+// then prunes leaves at a missed ancestor that the rebuilt tree would reach -- the ABI accepts any
+// BVH bytes, so this is checked, as plan_collapse does), when a leaf box is flat or inverted
+// (plan_collapse's condition), when the tree has fewer than 3 leaves, or when the host memory
+// for the plan cannot be had.
+std::vector<rt_dnode> rebuild_inner_impl(const std::vector<rt_dnode>& dn, int mode);
 std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn, int mode = 1) {
+    if (dn.size() <= RT_SMALL_TREE || dn.size() > RT_LINK_MAX_NODES || !boxes_nest(dn)) return {};
+    try {
+        return rebuild_inner_impl(dn, mode);
+    } catch (const std::bad_alloc&) {   // the walk keeps the uploaded tree
+        return {};
+    }
+}
+
+// The dynamic programme's ranges: up to RT_REBUILD_DP_LEAVES leaves (3 m x m doubles + an m x m
+// split table: 28 MB at 1024; scene 8 has 897 leaves), greedy splits above.
+#define RT_REBUILD_DP_LEAVES 1024
+
+std::vector<rt_dnode> rebuild_inner_impl(const std::vector<rt_dnode>& dn, int mode) {
     std::vector<rt_dnode> out;
     const size_t n = dn.size();
-    if (n <= RT_SMALL_TREE || n > RT_LINK_MAX_NODES) return out;
     std::vector<uint32_t> L;
     for (size_t k = 0; k < n; k++) {
         const rt_dnode& d = dn[k];
@@ -552,10 +577,10 @@ std::vector<rt_dnode> rebuild_inner(const std::vector<rt_dnode>& dn, int mode = 
     };
     out.resize(2 * m - 1);
     std::vector<rt_dnode> pre(m), suf(m);
-    // mode 2 (up to 4096 leaves): the split points of the tree whose inner boxes' areas sum least,
-    // by a dynamic programme over the ranges; otherwise each range split greedily
+    // mode 2 (up to RT_REBUILD_DP_LEAVES leaves): the split points of the tree whose inner boxes'
+    // areas sum least, by a dynamic programme over the ranges; otherwise each range split greedily
     std::vector<uint32_t> split;
-    if (mode == 2 && m <= 4096) {
+    if (mode == 2 && m <= RT_REBUILD_DP_LEAVES) {
         std::vector<double> A(m * m), C(m * m, 0.0), CT(m * m, 0.0);   // CT[j * m + i] = C[i * m + j]
         for (size_t i = 0; i < m; i++) {
             rt_dnode b = dn[L[i]];
@@ -1377,21 +1402,83 @@ void abort_comms(rt_ctx* c);
 template <class F>
 int group_body(rt_ctx* c, F&& body) {
     const int r = body();
-    const ncclResult_t e = rccl().GroupEnd();
+    ncclResult_t e = rccl().GroupEnd();
+    if (e == ncclInProgress && c->comm_nonblocking) e = ncclSuccess;   // completed by comm_wait
     if (r || e != ncclSuccess) abort_comms(c);
     if (r) return r;
     if (e != ncclSuccess) return set_err(c, RT_ERR_DEVICE, std::string("ncclGroupEnd: ") + rccl().GetErrorString(e));
     return RT_OK;
 }
 
+// Frees the context's communicators and whatever they still have queued: ncclCommAbort, or
+// ncclCommDestroy where the library lacks it (a communicator is never just dropped).
 void abort_comms(rt_ctx* c) {
     for (Device& d : c->devs) {
         if (!d.comm) continue;
         if (rccl().CommAbort) (void)rccl().CommAbort(d.comm);
+        else (void)rccl().CommDestroy(d.comm);
         d.comm = nullptr;
     }
     c->proc_comm = false;
+    c->comm_nonblocking = false;
     c->comm_tried = false;   // a multi-device context makes its communicators again on the next gather
+}
+
+// Deadlines of the one-process-per-GPU exchange.  A peer that never joins
+// (ncclCommInitRank) or never posts its matching Send / Recv would otherwise hold the host
+// forever; with a deadline the call returns RT_ERR_TIMEOUT after aborting the communicator,
+// which also ends its queued kernels, and the caller falls back or reports.
+using Clock = std::chrono::steady_clock;
+Clock::time_point comm_deadline(const rt_ctx* c) {
+    return c->comm_timeout_ms > 0 ? Clock::now() + std::chrono::milliseconds(c->comm_timeout_ms)
+                                  : Clock::time_point::max();
+}
+
+int comm_timeout(rt_ctx* c, const std::string& what) {
+    abort_comms(c);
+    return set_err(c, RT_ERR_TIMEOUT, what + ": no completion within " + std::to_string(c->comm_timeout_ms) +
+                                          " ms (the communicator was aborted; rt_comm_init again)");
+}
+
+// The state of a non-blocking communicator's last operation: RT_OK once it is no longer
+// ncclInProgress, RT_ERR_DEVICE (communicator aborted) on an asynchronous error, RT_ERR_TIMEOUT
+// past the deadline.  A blocking communicator has nothing to wait for.
+int comm_wait(rt_ctx* c, ncclComm_t comm, Clock::time_point deadline, const char* what) {
+    if (!c->comm_nonblocking || !rccl().CommGetAsyncError) return RT_OK;
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t e = rccl().CommGetAsyncError(comm, &st);
+        if (e != ncclSuccess) st = e;
+        if (st == ncclSuccess) return RT_OK;
+        if (st != ncclInProgress) {
+            abort_comms(c);
+            return set_err(c, RT_ERR_DEVICE, std::string(what) + ": " + rccl().GetErrorString(st));
+        }
+        if (Clock::now() >= deadline) return comm_timeout(c, what);
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// hipStreamSynchronize with the deadline: polls the stream (and the communicator's asynchronous
+// error) instead of blocking in the runtime.
+int stream_wait(rt_ctx* c, Device& d, Clock::time_point deadline, const char* what) {
+    for (;;) {
+        const hipError_t e = hipStreamQuery(d.stream);
+        if (e == hipSuccess) return RT_OK;
+        if (e != hipErrorNotReady) {
+            abort_comms(c);
+            return set_err(c, RT_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+        }
+        if (d.comm && c->comm_nonblocking && rccl().CommGetAsyncError) {
+            ncclResult_t st = ncclSuccess;
+            if (rccl().CommGetAsyncError(d.comm, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress) {
+                abort_comms(c);
+                return set_err(c, RT_ERR_DEVICE, std::string(what) + ": " + rccl().GetErrorString(st));
+            }
+        }
+        if (Clock::now() >= deadline) return comm_timeout(c, what);
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
 }
 
 // Multi-device context: device k's stripe block (local_rows x W, in its padded slot) into
@@ -1492,8 +1579,40 @@ int rt_comm_init(rt_ctx* c, const void* id, int rank, int world) {
     }
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
-    NCCLCHK(c, rccl().CommInitRank(&d.comm, world, uid, rank));
-    c->proc_comm = true;
+    const Clock::time_point deadline = comm_deadline(c);
+    if (rccl().CommInitRankConfig && rccl().CommGetAsyncError && rccl().CommAbort) {
+        // non-blocking: ncclCommInitRankConfig returns at once and the init is polled against the
+        // deadline, so a rank that never joins cannot hold this one
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        const ncclResult_t e = rccl().CommInitRankConfig(&d.comm, world, uid, rank, &cfg);
+        if (e != ncclSuccess && e != ncclInProgress) {
+            if (d.comm) (void)rccl().CommAbort(d.comm);
+            d.comm = nullptr;
+            return set_err(c, RT_ERR_DEVICE, std::string("ncclCommInitRankConfig: ") + rccl().GetErrorString(e));
+        }
+        c->comm_nonblocking = true;
+        c->proc_comm = true;
+        const int r = comm_wait(c, d.comm, deadline, "ncclCommInitRankConfig");
+        if (r) return r;
+    } else {
+        NCCLCHK(c, rccl().CommInitRank(&d.comm, world, uid, rank));
+        c->comm_nonblocking = false;
+        c->proc_comm = true;
+    }
+    return RT_OK;
+}
+
+int rt_comm_set_timeout(rt_ctx* c, int timeout_ms) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    if (timeout_ms < 0) return set_err(c, RT_ERR_INVALID_ARG, "rt_comm_set_timeout: negative timeout");
+    c->comm_timeout_ms = timeout_ms;
+    return RT_OK;
+}
+
+int rt_comm_abort(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    abort_comms(c);
     return RT_OK;
 }
 
@@ -1511,6 +1630,9 @@ int rt_gather_image(rt_ctx* c, float* rgba) {
     if (r) return r;
     HIPCHK(c, hipSetDevice(d.id));
     const int world = c->proc_world;
+    // every wait below ends by the context's deadline (rt_comm_set_timeout): on a non-blocking
+    // communicator the enqueue is polled (comm_wait), and the stream is polled, not synchronised
+    const Clock::time_point deadline = comm_deadline(c);
     // rank k sends its local_rows x W block (a bound image holds no more); rank 0 receives
     // it into slot k of the padded gather buffer
     const size_t slot = (size_t)d.padded_rows * c->width * 16;
@@ -1529,15 +1651,24 @@ int rt_gather_image(rt_ctx* c, float* rgba) {
             return RT_OK;
         });
         if (in_group) return in_group;
+        if ((r = comm_wait(c, d.comm, deadline, "ncclRecv group"))) return r;
         if (rt_launch_deinterleave(d.gather.ptr, d.full.ptr, c->width, c->height, world, c->stripe_rows,
                                    d.padded_rows, d.stream))
             return set_err(c, RT_ERR_DEVICE, "de-interleave kernel launch failed");
-        int r2 = d2h(c, d, rgba, d.full.ptr, (size_t)c->height * c->width * 16);
-        if (r2) return r2;
+        if ((r = stream_wait(c, d, deadline, "ncclRecv"))) return r;
+        if ((r = d2h(c, d, rgba, d.full.ptr, (size_t)c->height * c->width * 16))) return r;
     } else {
         const size_t n = (size_t)d.local_rows * c->width * 4;
-        if (n) NCCLCHK(c, rccl().Send(d.image_ptr, n, ncclFloat, 0, d.comm, d.stream));
-        HIPCHK(c, hipStreamSynchronize(d.stream));
+        if (n) {
+            ncclResult_t e = rccl().Send(d.image_ptr, n, ncclFloat, 0, d.comm, d.stream);
+            if (e == ncclInProgress && c->comm_nonblocking) e = ncclSuccess;
+            if (e != ncclSuccess) {   // a failed Send frees the communicator too
+                abort_comms(c);
+                return set_err(c, RT_ERR_DEVICE, std::string("ncclSend: ") + rccl().GetErrorString(e));
+            }
+            if ((r = comm_wait(c, d.comm, deadline, "ncclSend"))) return r;
+        }
+        if ((r = stream_wait(c, d, deadline, "ncclSend"))) return r;
     }
     c->gather_path = RT_GATHER_RCCL;
     return RT_OK;
@@ -2021,7 +2152,13 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             const std::vector<rt_dnode>& rb = use_r ? c->rb_dn : none;
             const std::vector<rt_dnode>& wdn = rb.empty() ? c->walk_dn : rb;
             std::vector<uint8_t> drop;
-            if (use_c) drop = plan_collapse(wdn, c->cam, c->width, c->height);
+            if (use_c) {
+                try {
+                    drop = plan_collapse(wdn, c->cam, c->width, c->height);
+                } catch (const std::bad_alloc&) {   // no plan: the walk keeps every node
+                    drop.clear();
+                }
+            }
             c->n_dropped = 0;
             for (uint8_t x : drop) c->n_dropped += x;
             const std::vector<uint8_t>* dp = c->n_dropped ? &drop : nullptr;

@@ -92,6 +92,8 @@ def _amd_protos(L):
     _proto(L, "rt_comm_init", i, vp, vp, i, i)
     _proto(L, "rt_gather_image", i, vp, c_float_p)
     _proto(L, "rt_gather_path", i, vp)
+    _proto(L, "rt_comm_set_timeout", i, vp, i)
+    _proto(L, "rt_comm_abort", i, vp)
     _proto(L, "rt_debug_eval_builtin", i, i, i, c_float_p, c_float_p, c_float_p, i)
     _proto(L, "rt_debug_threaded_bvh", i, vp, sz, vp, sz, c_int_p)
     _proto(L, "rt_debug_fast_tables", i, vp, sz, vp, sz, vp, sz, i, vp, sz, c_int_p,

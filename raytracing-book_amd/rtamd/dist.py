@@ -69,7 +69,7 @@ def _agree(ok, what):
         raise RuntimeError(f"native gather: {what} failed on some rank")
 
 
-def native_gather(ctx, rank, world):
+def native_gather(ctx, rank, world, timeout_ms=None):
     """The gather through the C ABI (rt_comm_init + rt_gather_image: RCCL sends to rank 0,
     de-interleave kernel there): rank 0 makes the communicator id, torch.distributed
     hands it to the other ranks and agrees, between the steps, that every rank got
@@ -78,7 +78,11 @@ def native_gather(ctx, rank, world):
     The agreements bound what one rank's failure can do to the others:
     rt_comm_init's argument checks are made on every rank before any rank enters
     ncclCommInitRank (a collective), and every rank's render is synchronised (rt_sync,
-    which reports a device fault) before any rank enters the Send / Recv group."""
+    which reports a device fault) before any rank enters the Send / Recv group.
+
+    `timeout_ms` bounds rt_comm_init and rt_gather_image on every rank
+    (rt_comm_set_timeout): a peer that never joins or never posts its half of the exchange
+    makes the call raise RTError(RT_ERR_TIMEOUT) with the communicator aborted, not block."""
     from . import render
     if world == 1:
         return ctx.read_image()
@@ -100,6 +104,8 @@ def native_gather(ctx, rank, world):
            and getattr(ctx, "world", world) == world, "the rt_comm_init preconditions")
     ok = True
     try:
+        if timeout_ms is not None:
+            ctx.comm_set_timeout(timeout_ms)
         ctx.comm_init(uid, rank, world)
     except Exception:  # noqa: BLE001 -- every rank raises in _agree
         ok = False

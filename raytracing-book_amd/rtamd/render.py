@@ -251,6 +251,15 @@ class RenderContext:
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         self._check(self._L.rt_comm_init(self._h, buf, int(rank), int(world)))
 
+    def comm_set_timeout(self, timeout_ms):
+        """rt_comm_set_timeout: deadline of comm_init / gather_image in ms (0 = none); past it the
+        call raises RTError(RT_ERR_TIMEOUT) with the communicator aborted."""
+        self._check(self._L.rt_comm_set_timeout(self._h, int(timeout_ms)))
+
+    def comm_abort(self):
+        """rt_comm_abort: abort the communicator and free its queued work."""
+        self._check(self._L.rt_comm_abort(self._h))
+
     def gather_image(self):
         """rt_gather_image: the full [H, W, 4] image on rank 0 (None on the other ranks)."""
         if self.rank == 0:

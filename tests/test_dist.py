@@ -226,3 +226,102 @@ def test_gather_single_rank_is_identity():
     block = torch.from_numpy(np.random.default_rng(0).random((16, 5, 4), dtype=np.float32))
     img = rdist.gather_image(block, 13, 1, 16)
     assert img.shape == (13, 5, 4) and np.array_equal(img, block[:13].numpy())
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+class _BlockingCtx(_FakeCtx):
+    """A context whose rt_gather_image never returns (a peer that never posts its half)."""
+
+    def gather_image(self):
+        import threading
+        self.calls.append("gather_image")
+        threading.Event().wait()
+
+
+def _hang_worker(rank, world, port, path, block):
+    try:
+        import types
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        rdist.init_from_env(backend="gloo")
+        import rtamd.render as R
+        R.comm_unique_id = lambda: bytes(range(128))
+        bench = _bench_module()
+        img = np.zeros((4, 3, 4), np.float32)
+        cls = _BlockingCtx if block else _FakeCtx
+        ctx = cls(rank, img if rank == 0 else None, world=world)
+        ctx.comm_set_timeout = lambda ms: ctx.calls.append(("timeout", ms))
+        out = {"metric": "m", "value": 6803.59, "unit": "Msamples/s", "n_gpus": world}
+        args = types.SimpleNamespace(comm_timeout_ms=1000, height=4, stripe_rows=8, png=None, fast_bvh=False,
+                                     gather_deadline=3.0)
+        with open(f"{path}.{rank}", "w") as f:
+            guard = bench.LineGuard(out, rank, args.gather_deadline, stream=f)
+            extra = bench.finish(args, None, ctx, None, rank, world, 0, None, 0)
+            guard.emit(extra)
+            dist.barrier()
+            dist.destroy_process_group()
+            guard.close()
+    except Exception as e:  # noqa: BLE001 -- reported through the file
+        with open(f"{path}.{rank}.err", "w") as f:
+            f.write(repr(e))
+        os._exit(3)
+
+
+def _run_hang(tmp_path, block):
+    import json
+    import time
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    path = str(tmp_path / "line")
+    t = time.perf_counter()
+    procs = [ctx.Process(target=_hang_worker, args=(r, world, port, path, block)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    took = time.perf_counter() - t
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    errs = [open(f"{path}.{r}.err").read() for r in range(world) if os.path.exists(f"{path}.{r}.err")]
+    assert not errs, errs
+    lines = [json.loads(x) for x in open(f"{path}.0").read().splitlines() if x.strip()]
+    rest = open(f"{path}.1").read()
+    return lines, rest, [p.exitcode for p in procs], took
+
+
+def test_bench_line_survives_a_gather_that_never_returns(tmp_path):
+    """rank 0's rt_gather_image blocks forever (its peer never posts).  The
+    bench's watchdog (LineGuard) still prints exactly one line with the timed value and
+    gather_path "timeout", and every rank leaves with status 0 well before any outer limit."""
+    lines, rest, codes, took = _run_hang(tmp_path, True)
+    assert len(lines) == 1, lines
+    assert lines[0]["value"] == 6803.59 and lines[0]["gather_path"] == "timeout", lines[0]
+    assert rest == "" and codes == [0, 0], (rest, codes)
+    assert took < 60, took
+
+
+def test_bench_line_once_when_the_gather_completes(tmp_path):
+    """The same harness with a gather that completes: one line, the native path's fields, no
+    watchdog line after it (close() stops the timer)."""
+    lines, rest, codes, _ = _run_hang(tmp_path, False)
+    assert len(lines) == 1, lines
+    ln = lines[0]
+    assert ln["value"] == 6803.59 and ln["gather_path"].startswith("rt_gather_image"), ln
+    assert ln["gather_native_error"] is None and ln["nan_pixels"] == 0, ln
+    assert rest == "" and codes == [0, 0], (rest, codes)
+
+
+def test_native_gather_sets_the_deadline_before_comm_init():
+    """native_gather hands timeout_ms to rt_comm_set_timeout before rt_comm_init (world 1 has no
+    communicator and reads the image)."""
+    c = _FakeCtx(0, np.zeros((2, 2, 4), np.float32), world=1)
+    assert rdist.native_gather(c, 0, 1, timeout_ms=5) is c.image and c.calls == ["read_image"]

@@ -211,3 +211,28 @@ def test_shading_threshold_by_kernel(gpu):
             imgs.append(c.read_image())
             c.close()
         assert bit_equal(imgs[0], imgs[1]) and bit_equal(imgs[0], imgs[2]), f"scene {sid}"
+
+
+@pytest.mark.parametrize("sid", [8, 0])
+def test_non_nesting_bvh_under_default_options(gpu, sid):
+    """an uploaded BVH whose inner boxes do not hold their children's (the ABI takes
+    any BVH bytes).  Inner nodes are shrunk to a small box around their centre, so the
+    reference's walk prunes their leaves for most rays; the inner-node rebuild and the collapse
+    (both on by default) must then stand down -- a rebuilt tree would reach those leaves, and
+    a medium's rand() draws would shift -- and the default render equals the oracle's walk of
+    the uploaded tree bit for bit."""
+    s = rtamd.Scene(sid, 64, 36, seed=1)
+    rec = np.frombuffer(s.buffers[1], dtype=[("box", "<f4", 6), ("l", "<u4"), ("r", "<u4")]).copy()
+    inner = [k for k in range(len(rec)) if rec[k]["l"] & 0xFFFF == 0 and rec[k]["r"] & 0xFFFF == 0]
+    assert len(inner) > 60
+    for k in inner[2:40:7]:
+        b = rec[k]["box"].astype(np.float64)
+        c, h = (b[0::2] + b[1::2]) / 2, (b[1::2] - b[0::2]) / 8
+        rec[k]["box"] = np.stack([c - h, c + h], axis=1).reshape(6).astype(np.float32)
+    s.buffers = dict(s.buffers)
+    s.buffers[1] = rec.tobytes()
+    case = type("Case", (), dict(scene=s, depth=5, uniforms=rtamd.spp_uniforms(4), frames=4))
+    ref = oracle(case)
+    out, info = render(case)
+    assert bit_equal(out, ref), mismatch_report(out, ref)
+    assert info["rebuilt"] == 0 and info["collapsed"] == 0, info

@@ -97,6 +97,34 @@ def test_process_communicator_gather(gpu):
     assert bit_equal(out, ref), mismatch_report(out, ref)
 
 
+def test_process_communicator_times_out_without_its_peer(gpu):
+    """rank 0 of a world-2 communicator whose rank 1 never joins.  With a
+    2 s deadline (rt_comm_set_timeout) rt_comm_init returns RT_ERR_TIMEOUT with the
+    communicator aborted, instead of blocking in ncclCommInitRank; the context still renders
+    and reads its stripes, and a gather asks for rt_comm_init again."""
+    import time
+    s = rtamd.Scene(8, 48, 27, seed=1)
+    ctx = rtamd.RenderContext(rank=0, world=2, stripe_rows=8)
+    ctx.upload_scene(s)
+    ctx.set_params(max_depth=5, spp=2)
+    ctx.resize(48, 27)
+    ctx.render(1, rtamd.frame_rand_factors(1, 0, 2))
+    ctx.comm_set_timeout(2000)
+    t = time.perf_counter()
+    with pytest.raises(rtamd.RTError, match="no completion within 2000 ms") as e:
+        ctx.comm_init(rtamd.comm_unique_id(), 0, 2)
+    took = time.perf_counter() - t
+    assert e.value.code == -6 and took < 30, (e.value, took)
+    with pytest.raises(rtamd.RTError, match="rt_comm_init"):
+        ctx.gather_image()
+    ctx.comm_abort()   # idempotent
+    blk = ctx.read_image()
+    ref = oracle_image(s, 2)
+    rows = rtamd.stripe_rows_of(27, 0, 2, 8)
+    ctx.close()
+    assert bit_equal(blk, ref[rows]), mismatch_report(blk, ref[rows])
+
+
 @pytest.mark.parametrize("w,h", [(1, 1), (7, 3), (65, 9), (3, 70), (129, 1)])
 def test_ragged_sizes(gpu, w, h):
     """Sizes that are not multiples of the 8x8 wave tile."""

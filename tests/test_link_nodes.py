@@ -322,15 +322,32 @@ def test_collapsed_walk_tests_the_same_leaves(sid):
     assert steps_coll != steps_full or nd == 0
 
 
-def test_collapse_keeps_a_tree_whose_boxes_do_not_nest():
-    """No collapse unless every child box lies inside its parent's (boxes_nest) and no box is flat."""
+@pytest.mark.parametrize("rebuild", [0, 1, 2])
+def test_collapse_keeps_a_tree_whose_boxes_do_not_nest(rebuild):
+    """No collapse unless every child box lies inside its parent's (boxes_nest) and no box is flat;
+    and no inner-node rebuild either: over a tree whose boxes do not nest the
+    reference's walk prunes leaves at a missed ancestor that a rebuilt tree would reach, so the
+    walk keeps the uploaded tree's links exactly."""
     rec = np.frombuffer(heap_bvh(64), dtype=[("box", "<f4", 6), ("l", "<u4"), ("r", "<u4")]).copy()
     rec[5]["box"] = [-2, 2, -1, 1, -1, 1]   # an inner node wider than its parent
     scene = rtamd.Scene(9, 64, 36, seed=1)
     scene.buffers = dict(scene.buffers)
     scene.buffers[1] = rec.tobytes()
-    _, drop, nd = collapse_links(scene)
+    links, drop, nd = collapse_links(scene, rebuild=rebuild)
     assert nd == 0 and not drop.any()
+    assert np.array_equal(links.view(np.uint32), links_of(rec.tobytes()).view(np.uint32))
+    # the nesting tree is rebuilt (the gate is the nesting, not the size)
+    if rebuild:
+        ok = np.frombuffer(heap_bvh(64), dtype=rec.dtype).copy()
+        ok["box"][63:] = [[-1 + j / 64, -1 + (j + 1) / 64, -1, 1, -1, 1] for j in range(64)]
+        links2, _, _ = collapse_links(scene_with_bvh(scene, ok.tobytes()), rebuild=rebuild)
+        assert not np.array_equal(links2.view(np.uint32), links_of(ok.tobytes()).view(np.uint32))
+
+
+def scene_with_bvh(scene, b):
+    scene.buffers = dict(scene.buffers)
+    scene.buffers[1] = b
+    return scene
 
 
 # ---- inner-node rebuild (option rebuild, round 5) -------------------------------------------------
