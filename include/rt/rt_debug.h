@@ -71,12 +71,18 @@ int rt_debug_box_records(const void* boxes, size_t nbytes, void* out, size_t out
 
 /* Diagnostic build of the render kernel with wave-level region timers and
  * active-lane counters (never used for timed numbers).  enable=1 switches the
- * context to it and zeroes the counters; read returns n <= 64 counters.
+ * context to it and zeroes the counters; enable=2 also records the leaf census
+ * (one record per wave leaf round: start cycle, cycles, workgroup | wave << 16 |
+ * walking lanes << 24, slot 0's and slot 1's lanes per prim type as bytes: sphere,
+ * quad, medium, box); read returns n <= 128 counters.  read_census copies the first
+ * device's census (per resident wave its record count, then *cap records of 5 words
+ * per wave); out may be NULL to query *needed (words), *waves and *cap.
  * The stats kernels exist only in the A/B build (librtamd_ab.so, built with
  * -DRT_AB_KNOBS); the release library returns RT_ERR_STATE. */
 struct rt_ctx;
 int rt_debug_enable_stats(struct rt_ctx* ctx, int enable);
 int rt_debug_read_stats(struct rt_ctx* ctx, unsigned long long* out, int n);
+int rt_debug_read_census(struct rt_ctx* ctx, unsigned int* out, size_t words, size_t* needed, int* waves, int* cap);
 
 /* Number of visible HIP devices (0 when none). */
 int rt_debug_device_count(void);

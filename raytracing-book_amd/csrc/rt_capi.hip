@@ -89,6 +89,8 @@ struct Device {
     DevBuf image;            // internal image
     DevBuf args;             // rt_kernel_args slot in device memory
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
+    DevBuf census;           // the stats twin's leaf census (rt_debug_enable_stats(ctx, 2))
+    int census_cap = 0, census_waves = 0;
     DevBuf counter;          // persistent-kernel work-unit counter [0] and fault word [1]
     DevBuf tile_done;        // ordered chunks: chunks published per 8x8 tile
     DevBuf samples;          // staged chunks: per-frame colours [frames][local pixels]
@@ -1738,7 +1740,7 @@ int rt_destroy(rt_ctx* c) {
         (void)hipSetDevice(d.id);
         (void)hipStreamSynchronize(d.stream);
         dev_free(d.nodes); dev_free(d.spheres); dev_free(d.quads); dev_free(d.boxes); dev_free(d.media);
-        dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.counter);
+        dev_free(d.lights); dev_free(d.image); dev_free(d.args); dev_free(d.stats); dev_free(d.census); dev_free(d.counter);
         dev_free(d.tile_done); dev_free(d.samples); dev_free(d.wbuf); dev_free(d.dquads); dev_free(d.dboxes);
         dev_free(d.finfo); dev_free(d.f2inner); dev_free(d.f2leaves); dev_free(d.links); dev_free(d.dboxc);
         dev_free(d.gather); dev_free(d.full); dev_free(d.perlin_pk); dev_free(d.sflags);
@@ -2375,6 +2377,9 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         }
         a.image = d.image_ptr;
         a.stats = (unsigned long long*)d.stats.ptr;
+        a.census = (unsigned*)d.census.ptr;
+        a.census_cap = d.census_cap;
+        a.census_waves = d.census_waves;
         a.local_rows = d.local_rows;
         a.rank = d.rank;
         a.world = d.world;
@@ -2828,8 +2833,11 @@ static int stats_twin(int v) {
     return 39;
 }
 
+// Leaf census records per resident wave (rt_debug_enable_stats(ctx, 2); tools/leaf_census.py)
+#define RT_CENSUS_CAP 2048
+
 int rt_debug_enable_stats(rt_ctx* c, int on) {
-    if (!c) return RT_ERR_INVALID_ARG;
+    if (!c || on < 0 || on > 2) return RT_ERR_INVALID_ARG;
 #ifndef RT_AB_KNOBS
     if (on) return set_err(c, RT_ERR_STATE, "the stats kernels are in the A/B build (librtamd_ab.so)");
 #endif
@@ -2837,10 +2845,23 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
         HIPCHK(c, hipSetDevice(d.id));
         HIPCHK(c, hipStreamSynchronize(d.stream));
         if (on && !d.stats.ptr) {
-            HIPCHK(c, hipMalloc(&d.stats.ptr, 64 * sizeof(unsigned long long)));
-            d.stats.bytes = 64 * sizeof(unsigned long long);
+            HIPCHK(c, hipMalloc(&d.stats.ptr, RT_STATS_N * sizeof(unsigned long long)));
+            d.stats.bytes = RT_STATS_N * sizeof(unsigned long long);
         }
         if (d.stats.ptr) HIPCHK(c, hipMemsetAsync(d.stats.ptr, 0, d.stats.bytes, d.stream));
+        if (on == 2 && !d.census.ptr) {
+            const int waves = rt_resident_waves();
+            const size_t bytes = ((size_t)waves + (size_t)waves * RT_CENSUS_CAP * RT_CENSUS_WORDS) * sizeof(unsigned);
+            HIPCHK(c, hipMalloc(&d.census.ptr, bytes));
+            d.census.bytes = bytes;
+            d.census_cap = RT_CENSUS_CAP;
+            d.census_waves = waves;
+        }
+        if (on != 2 && d.census.ptr) {
+            dev_free(d.census);
+            d.census_cap = d.census_waves = 0;
+        }
+        if (d.census.ptr) HIPCHK(c, hipMemsetAsync(d.census.ptr, 0, d.census.bytes, d.stream));
         HIPCHK(c, hipStreamSynchronize(d.stream));
     }
     if (on) {
@@ -2853,8 +2874,22 @@ int rt_debug_enable_stats(rt_ctx* c, int on) {
     return RT_OK;
 }
 
+int rt_debug_read_census(rt_ctx* c, unsigned* out, size_t words, size_t* needed, int* waves, int* cap) {
+    if (!c || c->devs.empty()) return RT_ERR_INVALID_ARG;
+    Device& d = c->devs[0];
+    const size_t n = d.census.bytes / sizeof(unsigned);
+    if (needed) *needed = n;
+    if (waves) *waves = d.census_waves;
+    if (cap) *cap = d.census_cap;
+    if (!out) return RT_OK;
+    if (words < n) return set_err(c, RT_ERR_LIMIT, "census buffer too small");
+    if (!n) return RT_OK;
+    HIPCHK(c, hipSetDevice(d.id));
+    return d2h(c, d, out, d.census.ptr, d.census.bytes);
+}
+
 int rt_debug_read_stats(rt_ctx* c, unsigned long long* out, int n) {
-    if (!c || !out || n <= 0 || n > 64) return RT_ERR_INVALID_ARG;
+    if (!c || !out || n <= 0 || n > RT_STATS_N) return RT_ERR_INVALID_ARG;
     std::memset(out, 0, sizeof(unsigned long long) * n);
     for (Device& d : c->devs) {
         if (!d.stats.ptr) continue;

@@ -41,10 +41,14 @@
 // the pooled link-walk kernel as one 1024-thread workgroup per CU (16 waves, 4 per SIMD, the
 // same as two workgroups of 512): one copy of the nodes per CU leaves room for the leaf
 // tests' sphere and box records.  The release kernels have no static LDS and take all 160 KB; the
-// stats twins (A/B library) keep 8 KB for their static counters (RT_LDS_BIG_STATS_BYTES), so their
+// stats twins (A/B library) keep 10 KB for their static counters (RT_LDS_BIG_STATS_BYTES), so their
 // plan may leave out the last table (rt_capi.hip: the LDS plan by variant)
 #define RT_LDS_BIG_BYTES (160 * 1024)
-#define RT_LDS_BIG_STATS_BYTES (152 * 1024)
+#define RT_LDS_BIG_STATS_BYTES (150 * 1024)
+// the leaf census record (stats twin): start cycle, cycles, workgroup | wave << 16 | walking lanes << 24,
+// slot 0's lanes per prim type (sphere, quad, medium, box: a byte each), slot 1's
+#define RT_CENSUS_WORDS 5
+#define RT_STATS_N 128   // counters rt_debug_read_stats can read (the kernels' ST_N <= 80)
 #define RT_LDS_NODE_BYTES (64 * 1024)   // threaded (meta-word) nodes in LDS when they fit
 
 // Threaded BVH node.  Traversal from node 0: on an AABB hit an inner node
@@ -111,6 +115,9 @@ struct rt_kernel_args {
     int rank, world, stripe_rows;
     int first_frame, n_frames;
     unsigned long long* stats;   // diagnostic counters (stats variant only)
+    unsigned* census;            // stats twin, leaf census (rt_debug_enable_stats(ctx, 2)): per resident wave its
+                                 // record count, then census_cap records of RT_CENSUS_WORDS words per wave
+    int census_cap, census_waves;
     int* tile_counter;           // persistent kernel: next work unit (zeroed per launch)
     // work split: unit = chunk * n_tiles + tile, chunk = frames [c*chunk_frames, ...) (ordered chunks)
     int n_chunks, chunk_frames;

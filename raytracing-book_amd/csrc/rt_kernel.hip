@@ -140,7 +140,19 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     unsigned long long t_prog = __builtin_amdgcn_s_memrealtime();
     uint32_t stored = 0, stored_seen = 0;   // wave-uniform: samples this wave stored
     uint32_t pass = 0;
+    // the stats twin's pass-part timers (ST_PASS_CYC ... ST_PTAIL_CYC): tq = the current part's start
+    unsigned long long tq = 0, tq0 = 0;
+#define RT_ST_PART(slot)                                  \
+    if (STATS) {                                          \
+        const unsigned long long tn_ = clock64();         \
+        st_add(st, (slot), tn_ - tq);                     \
+        tq = tn_;                                         \
+    }
     for (;;) {
+        if (STATS) {
+            tq0 = tq = clock64();
+            st_add(st, ST_PASS_IT, 1ull);
+        }
         if ((pass++ & 255u) == 0) {
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
             if (now - t_prog >= P.watchdog_ticks) {
@@ -152,6 +164,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                 t_prog = now;
             }
         }
+        RT_ST_PART(ST_WATCH_CYC)
         // fold the units whose samples are all stored, oldest first (ordered / one chunk)
         if (!staged) {
 #pragma unroll 1
@@ -191,10 +204,12 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                 }
             }
         }
+        RT_ST_PART(ST_FOLD_CYC)
         // claim samples for the FRESH lanes (compute.glsl:345-350); a new unit when the
         // pool's unit has none left
         bool fin = false;   // a sample stored in this pass (max_depth 0)
         for (;;) {
+            if (STATS) st_add(st, ST_CLAIM_IT, 1ull);
             const unsigned long long need = __ballot(status == RT_SM_FRESH);
             if (need == 0) break;
             if (next >= total_cur) {
@@ -202,8 +217,13 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                 const int o = staged ? 0 : cur ^ 1;
                 if (!staged && (o ? unit1 : unit0) >= 0) break;   // both slots in use: the FRESH lanes wait
                 int u = 0;
+                unsigned long long ta = STATS ? clock64() : 0;
                 if (lane == 0) u = atomicAdd(P.tile_counter, 1);
                 u = __builtin_amdgcn_readfirstlane(__shfl(u, 0));
+                if (STATS) {
+                    st_add(st, ST_ATOM_CYC, clock64() - ta);
+                    st_add(st, ST_UNIT_IT, 1ull);
+                }
                 if (u >= n_units) {
                     no_more = true;
                     break;
@@ -268,6 +288,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             next = min(next + (uint32_t)__popcll(need), total_cur);
             if (__ballot(fin)) break;   // count these before claiming more (below)
         }
+        RT_ST_PART(ST_CLAIM_CYC)
         // a new walk (bounce(): depth, a zero direction hits nothing, compute.glsl:226-229)
         if (status == RT_SM_BEGIN) {
             S.depth++;
@@ -287,14 +308,17 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
         // chains then issue as soon as their data is back, and the shading's long VALU runs (at
         // priority 0) fill the gaps -- scene 8 -3.1%, scene 0 -2.1%, scenes 6 / 7 -0.4 / -1.2%
         // (profiles/r04_setprio_combined_lib_ab.log; the walk alone at 1: scene 6 +0.6%)
+        RT_ST_PART(ST_BEGIN_CYC)
         __builtin_amdgcn_s_setprio(1);
         for (;;) {
+            unsigned long long th = STATS ? clock64() : 0;
             const unsigned long long tr = __ballot(status == RT_SM_TRACE);
             const int n_hit = __popcll(__ballot(status == RT_SM_HIT));
             if (STATS && tr) st_pred(st, status == RT_SM_FRESH, ST_RET_IT, ST_RET_LN);
             if (tr == 0 || n_hit >= batch || n_hit * 64 >= P.sm_frac * (n_hit + __popcll(tr))) break;
             const bool lane_exact = (inv.x == -INFINITY) || (inv.y == -INFINITY) || (inv.z == -INFINITY);
             const bool wave_exact = __ballot(status == RT_SM_TRACE && lane_exact) != 0;
+            if (STATS) st_add(st, ST_RHEAD_CYC, clock64() - th);
             if (status == RT_SM_TRACE) {
                 if (STATS) st_lanes(st, ST_ROUND_IT, ST_ROUND_LN);
                 unsigned long long t0 = STATS ? clock64() : 0;
@@ -320,13 +344,18 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0>(P, lf.x << 16, lf.y, S.o, S.d, inv, a,
                                                                              S.time, 0.001f, tmax, S.rf,
                                                   fx, fy, h, has, st);
-                    if (STATS) st_add(st, ST_LEAF_CYC, clock64() - t1);
+                    if (STATS) {
+                        const unsigned long long t2 = clock64();
+                        st_add(st, ST_LEAF_CYC, t2 - t1);
+                        if (P.census) census_leaf(P, gwave, lf.x, t1, t2, __popcll(tr), st);
+                    }
                     nx = lf.x >> 8;   // the leaf's skip node
                     if (nx == RT_LINK_NEXT_END) status = RT_SM_HIT;
                 }
             }
         }
         __builtin_amdgcn_s_setprio(0);
+        RT_ST_PART(ST_ROUNDS_CYC)
         // shade the HIT lanes together
         if (status == RT_SM_HIT) {
             unsigned long long ts = STATS ? clock64() : 0;
@@ -368,14 +397,20 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             }
             if (STATS) st_add(st, ST_SHADE_CYC, clock64() - ts);
         }
+        RT_ST_PART(ST_SHBLK_CYC)
         // the samples stored in this pass, per slot
         const unsigned long long f_all = __ballot(fin), f_one = __ballot(fin && up == 1);
         done0 += (uint32_t)__popcll(f_all & ~f_one);
         done1 += (uint32_t)__popcll(f_one);
         stored += (uint32_t)__popcll(f_all);
         // the end: no unit left to claim, every lane idle, every slot folded
+        if (STATS) {
+            RT_ST_PART(ST_PTAIL_CYC)
+            st_add(st, ST_PASS_CYC, tq - tq0);
+        }
         if (no_more && __ballot(status != RT_SM_FRESH) == 0 && (staged || (unit0 < 0 && unit1 < 0))) break;
     }
+#undef RT_ST_PART
 }
 
 // Persistent kernel: one resident grid; each workgroup stages the link-format BVH, the Perlin
@@ -401,6 +436,8 @@ __global__ void __launch_bounds__(BLOCK, MINW) render_persistent(const KP* __res
     render_stream<STATS, OPT, (OPT & RT_OPT_FD) != 0>(P, s_nodes, (int)blockIdx.x * (BLOCK / 64) + (tid >> 6), st);
     if (STATS) {
         st_add(st, ST_TOTAL, clock64() - t_begin);
+        const int gw = (int)blockIdx.x * (BLOCK / 64) + (tid >> 6);
+        if (P.census && (tid & 63) == 0 && gw < P.census_waves) P.census[gw] = (unsigned)st[ST_CEN_N];
         __syncthreads();
         if (tid < ST_N) {
             unsigned long long v = 0;

@@ -90,9 +90,17 @@ enum {
     // shading (round 5): wave-cycles of its parts -- the hit record, the material's scatter, the
     // mixture pdf, the texture lookups -- and the material blocks' executions and lanes
     ST_SH_HIT_CYC, ST_SH_SCAT_CYC, ST_SH_MIX_CYC, ST_SH_TEX_CYC, ST_SH_LAM_IT, ST_SH_LAM_LN, ST_SH_ISO_IT,
-    ST_SH_ISO_LN, ST_SH_MET_IT, ST_SH_MET_LN, ST_SH_DIE_IT, ST_SH_DIE_LN, ST_N
+    ST_SH_ISO_LN, ST_SH_MET_IT, ST_SH_MET_LN, ST_SH_DIE_IT, ST_SH_DIE_LN,
+    // render_stream's scheduling (round 6): passes of its loop and the wave-cycles
+    // of each part of a pass -- the watchdog check, the unit folds, the claim loop (which holds
+    // START), its iterations, units claimed and the unit counter's atomic, the new walks' set-up,
+    // the rounds (which hold NODE and LEAF) and their loop heads, the shading block (SHADE's
+    // first-lane timer runs inside it) and the pass tail; the leaf census' per-wave record count
+    ST_PASS_IT, ST_PASS_CYC, ST_WATCH_CYC, ST_FOLD_CYC, ST_CLAIM_CYC, ST_CLAIM_IT, ST_UNIT_IT, ST_ATOM_CYC,
+    ST_BEGIN_CYC, ST_ROUNDS_CYC, ST_RHEAD_CYC, ST_SHBLK_CYC, ST_PTAIL_CYC, ST_CEN_N, ST_N
 };
-static_assert(ST_N <= 64, "rt_debug_read_stats reads 64 counters");
+// 16 waves x ST_N x 8 B of static LDS in a 1024-thread stats twin: <= 10 KB (RT_LDS_BIG_STATS_BYTES)
+static_assert(ST_N <= 80, "the stats twins' static counters fit 10 KB per 1024-thread workgroup");
 __device__ __forceinline__ bool first_active_lane() {
     unsigned long long m = __ballot(1);
     return (unsigned)__lane_id() == (unsigned)(__ffsll((long long)m) - 1);
@@ -112,6 +120,32 @@ __device__ __forceinline__ void st_pred(unsigned long long* st, bool pred, int i
     if (m && first_active_lane()) {
         atomicAdd(&st[it_slot], 1ull);
         atomicAdd(&st[ln_slot], (unsigned long long)__popcll(m));
+    }
+}
+
+// The leaf census (stats twin with P.census): one record per wave leaf round -- when it started,
+// how long it took, which wave, how many lanes were walking, and per prim type how many lanes
+// hold a slot-0 / slot-1 test -- so tools/leaf_census.py can count what a workgroup-wide queue
+// per prim type could have pooled.  Called by the lanes at a leaf (the first one writes).
+__device__ __forceinline__ void census_leaf(const KP& P, int gwave, uint32_t types, unsigned long long t0,
+                                            unsigned long long t1, int walking, unsigned long long* st) {
+    const uint32_t a = types & 7u, b = (types >> 4) & 0xFu;
+    uint32_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int k = 1; k <= 4; k++) {
+        s0 |= (uint32_t)__popcll(__ballot(a == (uint32_t)k)) << (8 * (k - 1));
+        s1 |= (uint32_t)__popcll(__ballot(b == (uint32_t)k)) << (8 * (k - 1));
+    }
+    if (first_active_lane()) {
+        const unsigned long long i = atomicAdd(&st[ST_CEN_N], 1ull);
+        if (gwave < P.census_waves && i < (unsigned long long)P.census_cap) {
+            unsigned* r = P.census + P.census_waves + ((size_t)gwave * P.census_cap + i) * RT_CENSUS_WORDS;
+            r[0] = (unsigned)t0;
+            r[1] = (unsigned)(t1 - t0);
+            r[2] = (unsigned)blockIdx.x | ((unsigned)(threadIdx.x >> 6) << 16) | ((unsigned)walking << 24);
+            r[3] = s0;
+            r[4] = s1;
+        }
     }
 }
 

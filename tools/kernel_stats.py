@@ -17,7 +17,9 @@ NAMES = ["TOTAL", "START_CYC", "START_IT", "START_LN", "NODE_CYC", "NODE_IT", "N
          "SPH_CYC", "QUAD_CYC", "BOX_CYC", "MED_CYC", "TRACE_IT", "TRACE_LN", "ROUND_IT", "ROUND_LN",
          "RET_IT", "RET_LN", "SPH_SM", "QUAD_SM", "BOX_SM", "MED_SM", "NODE_SM",
          "SH_HIT_CYC", "SH_SCAT_CYC", "SH_MIX_CYC", "SH_TEX_CYC", "SH_LAM_IT", "SH_LAM_LN", "SH_ISO_IT", "SH_ISO_LN",
-         "SH_MET_IT", "SH_MET_LN", "SH_DIE_IT", "SH_DIE_LN"]
+         "SH_MET_IT", "SH_MET_LN", "SH_DIE_IT", "SH_DIE_LN",
+         "PASS_IT", "PASS_CYC", "WATCH_CYC", "FOLD_CYC", "CLAIM_CYC", "CLAIM_IT", "UNIT_IT", "ATOM_CYC",
+         "BEGIN_CYC", "ROUNDS_CYC", "RHEAD_CYC", "SHBLK_CYC", "PTAIL_CYC", "CEN_N"]
 
 
 def main():
@@ -46,8 +48,8 @@ def main():
     assert L.rt_debug_enable_stats(ctx._h, 1) == 0
     ctx.render(1, rtamd.frame_rand_factors(1, 0, a.frames))
     ctx.sync()
-    buf = (ctypes.c_ulonglong * 64)()
-    assert L.rt_debug_read_stats(ctx._h, buf, 64) == 0
+    buf = (ctypes.c_ulonglong * 128)()
+    assert L.rt_debug_read_stats(ctx._h, buf, 128) == 0
     v = {n: buf[i] for i, n in enumerate(NAMES)}
     tot = v["TOTAL"] or 1
     samples = a.width * a.height * a.frames
@@ -75,6 +77,24 @@ def main():
     if v["ROUND_IT"]:
         print(f"  rounds with retired lanes: {v['RET_IT'] / v['ROUND_IT'] * 100:5.1f}% of rounds, "
               f"{v['RET_LN'] / (64.0 * v['ROUND_IT']) * 100:5.1f}% of lane-rounds retired (unit tails)")
+    if v["PASS_IT"]:
+        # render_stream's passes (round 6): each part's wave-cycles; the claim loop holds START, the
+        # rounds hold NODE and LEAF, the shading block holds SHADE (its first-lane timer)
+        pc = v["PASS_CYC"]
+        print(f"  passes {v['PASS_IT']:.3e} ({v['PASS_IT'] / max(v['ROUND_IT'], 1):.2f} per round), "
+              f"{100.0 * pc / tot:5.1f}% of wave-cycles inside passes; parts, % of wave-cycles:")
+        parts = [("watchdog", v["WATCH_CYC"]), ("unit folds", v["FOLD_CYC"]),
+                 ("claim loop - START", v["CLAIM_CYC"] - v["START_CYC"]), ("  of it the unit atomic", v["ATOM_CYC"]),
+                 ("new walks' set-up", v["BEGIN_CYC"]),
+                 ("rounds - NODE - LEAF", v["ROUNDS_CYC"] - v["NODE_CYC"] - v["LEAF_CYC"]),
+                 ("  of it the loop heads", v["RHEAD_CYC"]),
+                 ("shading block - SHADE", v["SHBLK_CYC"] - v["SHADE_CYC"]), ("pass tail", v["PTAIL_CYC"]),
+                 ("outside passes", tot - pc)]
+        for name, c in parts:
+            print(f"    {name:24s} {100.0 * c / tot:5.1f}%")
+        named = v["START_CYC"] + v["NODE_CYC"] + v["LEAF_CYC"] + v["SHADE_CYC"]
+        print(f"  START+NODE+LEAF+SHADE {100.0 * named / tot:5.1f}%; claim-loop iterations {v['CLAIM_IT'] / max(v['PASS_IT'], 1):.2f}"
+              f" per pass, units {v['UNIT_IT']:.3e}, unit atomic {v['ATOM_CYC'] / max(v['UNIT_IT'], 1):.0f} cycles each")
     print("raw", v)
 
 
