@@ -561,9 +561,19 @@ float scattering_pdf(v3 normal, v3 scatter_dir, int material_val) {   // :111-12
 bool near_zero(v3 v) { const float s = 1e-8f; return fabsf(v.x) < s && fabsf(v.y) < s && fabsf(v.z) < s; }
 
 void metal_scatter(Inv& I, v3& ray_dir, v3 normal, float fuzz) {   // :12-15
+#if defined(RT_PROBE_METAL) && RT_PROBE_METAL == 1
+    // probe (tools/scene8_residual_probe.py, never the shipped oracle): the book's earlier form,
+    // reflect(unit(dir)) + fuzz * random_in_unit_sphere (random.glsl's rejection loop)
+    v3 n = g_reflect(g_normalize(ray_dir), normal);
+    ray_dir = add3(n, scale3(rand_vec_in_unit_sphere(I), fuzz));
+#elif defined(RT_PROBE_METAL) && RT_PROBE_METAL == 2
+    // probe: the reflected direction left unnormalised before the fuzz is added
+    ray_dir = add3(g_reflect(ray_dir, normal), scale3(rand_unit_vec(I), fuzz));
+#else
     ray_dir = g_reflect(ray_dir, normal);
     v3 n = g_normalize(ray_dir);
     ray_dir = add3(n, scale3(rand_unit_vec(I), fuzz));
+#endif
 }
 
 float reflectance(float cos_theta, float eta) {   // :17-22

@@ -2220,6 +2220,12 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     const int n_box = (int)(c->host_buf[RT_BIND_BOXES].size() / sizeof(rt_box));
     const int n_med = (int)(c->host_buf[RT_BIND_MEDIA].size() / sizeof(rt_medium));
     a.n_media = n_med;
+    a.media_sph = 1;
+    for (int k = 0; k < n_med; k++) {
+        rt_medium m;
+        std::memcpy(&m, c->host_buf[RT_BIND_MEDIA].data() + k * sizeof(rt_medium), sizeof m);
+        if (m.boundary_type != RT_MODEL_SPHERE) a.media_sph = 0;
+    }
     a.n_sph_lds = n_sph;
     a.n_box_lds = n_box;
     a.box_all_cmp = (c->compact_boxes && n_box > 0 && c->n_boxc_ok == n_box) ? 1 : 0;

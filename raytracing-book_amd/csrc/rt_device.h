@@ -150,6 +150,7 @@ struct rt_kernel_args {
     int perlin_packed;           // 1: LDS holds the packed table perlin_pk (256 float4), not the texture
     const float4* perlin_pk;     // the packed Perlin table (rt_capi.hip rt_upload_texture), or nullptr
     int n_media;
+    int media_sph;               // every medium's boundary is a sphere (or there is none): RT_OPT_STD kernels
     int media_lds;               // float4 offset of the media records + sphere boundaries in LDS (3 float4
                                  // per medium, after the Perlin table), or -1
     int sph_lds;                 // float4 offset of the spheres' intersection halves (A, B) in LDS, or -1

@@ -97,7 +97,9 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     constexpr bool TL = (OPT & RT_OPT_TL) != 0;
     constexpr bool BOXC = (OPT & RT_OPT_BOXC) != 0;
     const int lane = threadIdx.x & 63;
-    const bool staged = P.samples != nullptr;
+    constexpr bool STD = (OPT & RT_OPT_STD) != 0;
+    const bool staged = STD || P.samples != nullptr;
+    const bool sparse = STD || P.sflags != nullptr;   // (staged launches)
     const int tiles_x = (P.width + 7) >> 3;
     const int n_tiles = tiles_x * ((P.local_rows + 7) >> 3);
     const int n_units = n_tiles * P.n_chunks;
@@ -274,7 +276,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     if (P.max_depth <= 0) {   // the loop never runs: final_color vec3(0)
                         const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                         if (staged) {
-                            if (P.sflags) P.sflags[dst] = 0;   // sparse: a zero colour is its clear flag
+                            if (sparse) P.sflags[dst] = 0;   // sparse: a zero colour is its clear flag
                             else P.samples[dst] = z4;
                         } else {
                             wbase[(size_t)up * slot_f4 + dst] = z4;
@@ -341,7 +343,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     uint2 lf;
                     if (gleaf) lf = ldg_u2(gleaves + (nx & 0x7FFFFFFFu));
                     else lf = leaves[nx & 0x7FFFFFFFu];
-                    leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0>(P, lf.x << 16, lf.y, S.o, S.d, inv, a,
+                    leaf_prims_t<STATS, FD, BOXC, (OPT & RT_OPT_SPAIR) != 0, STD>(P, lf.x << 16, lf.y, S.o, S.d, inv, a,
                                                                              S.time, 0.001f, tmax, S.rf,
                                                   fx, fy, h, has, st);
                     if (STATS) {
@@ -362,7 +364,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             if (STATS) st_lanes(st, ST_SHADE_IT, ST_SHADE_LN);
             v3 cur3;
             h.t = tmax;   // the accepted hit's t (unused on a miss)
-            bool done = after_trace<BOXC, STATS>(P, S, h, has, fx, fy, cur3, st);
+            bool done = after_trace<BOXC, STATS, STD>(P, S, h, has, fx, fy, cur3, st);
             if (!done && S.depth >= P.max_depth) {   // the loop is exhausted: final_color stays vec3(0)
                 cur3 = mk3s(0.0f);
                 done = true;
@@ -380,7 +382,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                     // sparse staging (P.sflags): every sample writes one flag byte, and only a colour
                     // that is not exactly (+0, +0, +0) is stored; fold_kernel reads a clear flag as
                     // that zero colour -- the same values, so the same running mean
-                    if (P.sflags) {
+                    if (sparse) {
                         const bool nz = (__float_as_uint(cur3.x) | __float_as_uint(cur3.y) | __float_as_uint(cur3.z)) != 0u;
                         P.sflags[dst] = nz ? 1 : 0;
                         if (nz) P.samples[dst] = c4;
@@ -640,15 +642,25 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
 #define RT_KERNEL(BLOCK, OPT) launch_persistent(render_persistent<4, false, BLOCK, OPT>, BLOCK, lds, a, d, st)
 #endif
     int rc = -1;
+    // the default launch's configuration (RT_OPT_STD) holds: the kernels with it compiled in
+    const bool std_cfg = a.samples && a.sflags && a.media_sph &&
+                         (a.n_sph_lds == 0 || (a.sph_lds >= 0 && a.sph_mat_lds >= 0)) &&
+                         (a.n_media == 0 || a.media_lds >= 0) && (a.n_box_lds == 0 || a.box_cmp_lds >= 0) &&
+                         (!a.box_all_cmp || (a.leaf_pf && a.box_mat_lds >= 0)) && a.tex_lds >= 0;
     // the link shapes x (shared-reciprocal division | plain) x (compact boxes | full box records)
 #define RT_LINK4(BLOCK, OPT)                                                                                 \
-    (a.fastdiv ? (a.box_all_cmp ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_BOXC) : RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD)) \
+    (a.fastdiv ? (a.box_all_cmp ? (std_cfg ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_BOXC | RT_OPT_STD)            \
+                                           : RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_BOXC))                         \
+                                : (std_cfg ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_STD)                            \
+                                           : RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD)))                                      \
                : (a.box_all_cmp ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_BOXC) : RT_KERNEL(BLOCK, (OPT))))
     // ... and, for a scene whose leaves are mostly sphere pairs (a.sph_pairs), without compact boxes
 #define RT_LINK4S(BLOCK, OPT)                                                                                 \
     ((a.sph_pairs == 2 && a.box_all_cmp && a.fastdiv) ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_BOXC | RT_OPT_SPAIR) : \
     (a.sph_pairs && !a.box_all_cmp)                                                                          \
-         ? (a.fastdiv ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_SPAIR) : RT_KERNEL(BLOCK, (OPT) | RT_OPT_SPAIR)) \
+         ? (a.fastdiv ? (std_cfg ? RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_SPAIR | RT_OPT_STD)                      \
+                                 : RT_KERNEL(BLOCK, (OPT) | RT_OPT_FD | RT_OPT_SPAIR))                                \
+                      : RT_KERNEL(BLOCK, (OPT) | RT_OPT_SPAIR))                                                       \
          : RT_LINK4(BLOCK, OPT))
     switch (shape) {
         case LINK_LDS:

@@ -29,6 +29,13 @@ typedef rt_kernel_args KP;
 #define RT_OPT_TL 16    // with RT_OPT_STREAM: two-level walk (top levels in LDS, the rest of the nodes global)
 #define RT_OPT_BOXC 32  // with RT_OPT_STREAM: every box has a compact record (box_test_compact), no full box test
 #define RT_OPT_SPAIR 64 // with RT_OPT_STREAM: leaves of two spheres tested at once (leaf_prims_t; most leaves are)
+#define RT_OPT_STD 128  // the default launch's configuration, compiled in (rt_launch_render std_config takes these
+                        // kernels when it holds): staged chunks with sparse staging (P.samples, P.sflags), every
+                        // medium bounded by a sphere (P.media_sph; no out-of-line boundary call), the leaf and
+                        // shading tables in LDS (spheres, media, box records, sphere materials, texture
+                        // descriptors) and with RT_OPT_BOXC the compact boxes' materials and the leaf record
+                        // prefetch (P.leaf_pf: the leaf stage holds only the prefetched forms).  Fewer wave-uniform
+                        // flags live through the rounds: the C3 kernel 128 -> 117 VGPRs, SGPR spills 34 -> 0
 
 // The kernels' dynamic LDS (render_persistent stages the BVH there, then the
 // Perlin table and the media records when P.perlin_lds / P.media_lds >= 0).
@@ -479,7 +486,7 @@ __device__ __forceinline__ bool medium_tail(float neg_inv_density, float t1, flo
 
 // medium_test on the medium's LDS record already loaded (R0 = boundary idx, type, -1/density, phase;
 // R1, R2 = its sphere boundary's A, B when the boundary is a sphere): the same operations.
-template <bool FD = false>
+template <bool FD = false, bool MSPH = false>
 __device__ __forceinline__ bool medium_test_rec(const KP& P, float4 R0, float4 R1, float4 R2, v3 o, v3 d, float a,
                                                 float time, float tmin, float tmax, float& rf, float px, float py,
                                                 float& t) {
@@ -490,7 +497,7 @@ __device__ __forceinline__ bool medium_test_rec(const KP& P, float4 R0, float4 R
     m.neg_inv_density = R0.z;
     m.phase_material = __float_as_int(R0.w);
     m.texture_id = 0;
-    if (m.boundary_type == RT_MODEL_SPHERE) {
+    if (MSPH || m.boundary_type == RT_MODEL_SPHERE) {   // MSPH: every medium's boundary is a sphere
         if (!sphere_bounds(R1, R2, o, d, a, time, t1, t2, FD)) return false;
     } else if (!medium_bounds(P, m, o, d, a, time, t1, t2)) {
         return false;
@@ -499,12 +506,12 @@ __device__ __forceinline__ bool medium_test_rec(const KP& P, float4 R0, float4 R
 }
 
 // hitting.glsl:162-193 — returns the hit distance t.
-template <bool FD = false>
+template <bool FD = false, bool STD = false>
 __device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, float a, float time, float tmin,
                                             float tmax, float& rf, float px, float py, float& t) {
     float t1, t2;
     rt_medium m;
-    if (P.media_lds >= 0) {   // the record and its sphere boundary from LDS (render_persistent)
+    if (STD || P.media_lds >= 0) {   // the record and its sphere boundary from LDS (render_persistent)
         const float4* r = rt_dyn_lds + P.media_lds + 3 * idx;
         const float4 R0 = r[0];
         m.boundary_idx = __float_as_int(R0.x);
@@ -512,7 +519,7 @@ __device__ __forceinline__ bool medium_test(const KP& P, int idx, v3 o, v3 d, fl
         m.neg_inv_density = R0.z;
         m.phase_material = __float_as_int(R0.w);
         m.texture_id = 0;
-        if (m.boundary_type == RT_MODEL_SPHERE) {
+        if (STD || m.boundary_type == RT_MODEL_SPHERE) {
             if (!sphere_bounds(r[1], r[2], o, d, a, time, t1, t2, FD)) return false;
         } else if (!medium_bounds(P, m, o, d, a, time, t1, t2)) {
             return false;
@@ -590,7 +597,7 @@ __device__ __forceinline__ bool aabb_pk(float4 n0, float4 n1, v3 o, v3 inv, floa
 
 // The two prims of a leaf (compute.glsl:247-256), left then right.
 // FD: the shared-reciprocal divisions (rcp_nr / div_nr; FD kernels only).
-template <bool STATS, bool FD, bool BOXC = false, bool SPAIR = false>
+template <bool STATS, bool FD, bool BOXC = false, bool SPAIR = false, bool STD = false>
 __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_t prims, v3 o, v3 d, v3 inv, float a,
                                              float time, float tmin, float& tmax, float& rf, float px, float py, Hit& h,
                                              bool& has, unsigned long long* st) {
@@ -603,7 +610,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
     // Only in the SPAIR kernels (scenes whose leaves are mostly sphere pairs, rt_capi.hip): where
     // most lanes hold other leaves, the extra block costs more than it saves (scene 8 +1%, and
     // the code alone scene 6 +1.3%); scene 0 -6.1%.
-    if (SPAIR && !STATS && P.sph_lds >= 0 && ((meta >> 16) & 0xFFu) == (RT_MODEL_SPHERE | (RT_MODEL_SPHERE << 4))) {
+    if (SPAIR && !STATS && (STD || P.sph_lds >= 0) && ((meta >> 16) & 0xFFu) == (RT_MODEL_SPHERE | (RT_MODEL_SPHERE << 4))) {
         const int i0 = (int)(prims & 0xFFFFu), i1 = (int)(prims >> 16);
         const float4* r0 = rt_dyn_lds + P.sph_lds + 2 * i0;
         const float4* r1 = rt_dyn_lds + P.sph_lds + 2 * i1;
@@ -670,7 +677,8 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
         // every lane before the type blocks, so the blocks do not each wait on their own LDS
         // round trip.  (A sphere's third float4 is its successor's A, or the next table's first:
         // in LDS, unused.)  The same values reach the same tests.
-        const bool pf = BOXC && P.leaf_pf;   // wave-uniform
+        // STD kernels (RT_OPT_STD): known on, the other forms compiled out
+        const bool pf = BOXC && (STD || P.leaf_pf);   // wave-uniform
         float4 q0, q1, q2;
         if (pf) {
             const int off = ty == RT_MODEL_SPHERE ? P.sph_lds + 2 * ix
@@ -685,7 +693,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
         if (ty == RT_MODEL_SPHERE) {
             if (pf) {
                 hit = sphere_t_ab(q0, q1, time, o, d, a, tmin, tmax, t, fd, fd ? rcp_nr(a) : 0.0f);
-            } else if (P.sph_lds >= 0) {   // the record's intersection half from LDS (render_persistent)
+            } else if (STD || P.sph_lds >= 0) {   // the record's intersection half from LDS (render_persistent)
                 const float4* r = rt_dyn_lds + P.sph_lds + 2 * ix;
                 hit = sphere_t_ab(r[0], r[1], time, o, d, a, tmin, tmax, t, fd, fd ? rcp_nr(a) : 0.0f);
             } else {
@@ -710,7 +718,7 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
                 r0 = q0;
                 r1 = q1;
                 r2 = q2;
-            } else if (P.box_cmp_lds >= 0) {
+            } else if (STD || P.box_cmp_lds >= 0) {
                 const float4* cr = rt_dyn_lds + P.box_cmp_lds + RT_BOXC_F4 * ix;
                 r0 = cr[0];
                 r1 = cr[1];
@@ -738,8 +746,8 @@ __device__ __forceinline__ void leaf_prims_t(const KP& P, uint32_t meta, uint32_
             if (hit) { h.uv_kind_idx = 2 << 16; h.uv_a = al; h.uv_b = be; }
             if (STATS) st_add(st, ST_BOX_CYC, clock64() - c0);
         } else if (ty == RT_MODEL_CONSTANT_MEDIUM) {
-            hit = pf ? medium_test_rec<FD>(P, q0, q1, q2, o, d, a, time, tmin, tmax, rf, px, py, t)
-                     : medium_test<FD>(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
+            hit = pf ? medium_test_rec<FD, STD>(P, q0, q1, q2, o, d, a, time, tmin, tmax, rf, px, py, t)
+                     : medium_test<FD, STD>(P, ix, o, d, a, time, tmin, tmax, rf, px, py, t);
             if (STATS) st_add(st, ST_MED_CYC, clock64() - c0);
         }
         if (hit) {
@@ -880,8 +888,9 @@ __device__ __forceinline__ void texel_in(const rt_dtex& T, int x, int y, float o
 }
 // texel() of slot `slot` through the LDS shading table when it is staged (P.tex_lds: the slot's
 // (w, h, is_float, texel offset); the same words as the texture), else from global memory
+template <bool STD = false>
 __device__ __forceinline__ void texel_slot(const KP& P, int slot, int x, int y, float out[3]) {
-    if (P.tex_lds >= 0) {
+    if (STD || P.tex_lds >= 0) {
         const float4 dsc = rt_dyn_lds[P.tex_lds + slot];
         const int w = __float_as_int(dsc.x), h = __float_as_int(dsc.y), off = __float_as_int(dsc.w);
         if (off >= 0) {
@@ -1034,13 +1043,14 @@ __device__ __forceinline__ v2 sphere_uv(v3 p) {
     return r;
 }
 
+template <bool STD = false>
 __device__ __forceinline__ v2 resolve_uv(const KP& P, const UvSrc& s, float time) {
     int kind = s.kind_idx >> 16;
     if (kind == 2) { v2 r = {s.a, s.b}; return r; }
     if (kind == 1) {
         const int si = s.kind_idx & 0xFFFF;
         float4 A, B;
-        if (P.sph_mat_lds >= 0) {   // the shading tables are on: the sphere's (A, B) from LDS
+        if (STD || P.sph_mat_lds >= 0) {   // the shading tables are on: the sphere's (A, B) from LDS
             A = rt_dyn_lds[P.sph_lds + 2 * si];
             B = rt_dyn_lds[P.sph_lds + 2 * si + 1];
         } else {
@@ -1056,7 +1066,7 @@ __device__ __forceinline__ v2 resolve_uv(const KP& P, const UvSrc& s, float time
 }
 
 // texture.glsl:112-132
-template <bool PK_INLINE = false>
+template <bool PK_INLINE = false, bool STD = false>
 __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvSrc& uvs, float time) {
 #ifdef RT_AB_KNOBS
     if (P.debug_flags & 4) return mk3s(0.5f);   // ablation only (A/B build): every texture a constant, never exact
@@ -1067,17 +1077,17 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
     const rt_dtex& T = P.tex[index & 7];
     float t[3];
     if (type == RT_TEXTYPE_SOLID) {
-        texel_slot(P, index & 7, detail_i, 0, t);
+        texel_slot<STD>(P, index & 7, detail_i, 0, t);
         return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_CHECKER) {   // :6-17
         int pix = detail_i * 3;
-        texel_slot(P, index & 7, pix + 2, 0, t);
+        texel_slot<STD>(P, index & 7, pix + 2, 0, t);
         float scale = t[0];
         float inv_scale = 1.0f / scale;
         v3 q = scale3(p, inv_scale);
         int s = rt_f2i(q.x) + rt_f2i(q.y) + rt_f2i(q.z);
-        texel_slot(P, index & 7, (s % 2 == 0) ? pix : pix + 1, 0, t);
+        texel_slot<STD>(P, index & 7, (s % 2 == 0) ? pix : pix + 1, 0, t);
         return mk3(t[0], t[1], t[2]);
     }
     if (type == RT_TEXTYPE_PERLIN) {    // :79-94
@@ -1100,7 +1110,7 @@ __device__ __forceinline__ v3 texture_color(const KP& P, v3 p, int id, const UvS
         if (P.debug_flags & 2) return mk3s(0.5f);   // ablation only (A/B build, RT_DEBUG_FLAGS), never exact
 #endif
         if (!T.data || T.w <= 0 || T.h <= 0) return mk3s(0.0f);
-        v2 uv = resolve_uv(P, uvs, time);
+        v2 uv = resolve_uv<STD>(P, uvs, time);
         float x = uv.x * (float)T.w - 0.5f;
         float y = uv.y * (float)T.h - 0.5f;
         float fx = floorf(x), fy = floorf(y);
@@ -1234,7 +1244,9 @@ struct Path {
 
 // The shading half of ray_color's loop body (compute.glsl:310-339) for a hit.
 // Returns true when the path ended, with its color in `result`.
-template <bool PK_INLINE = false, bool STATS = false>
+// STD (RT_OPT_STD kernels): the shading tables are staged -- every sphere's, and with PK_INLINE (the
+// compact-box kernels) every box's; the texture descriptors
+template <bool PK_INLINE = false, bool STATS = false, bool STD = false>
 __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float px, float py, v3& result,
                                       unsigned long long* st = nullptr) {
     unsigned long long c0 = STATS ? clock64() : 0;
@@ -1249,7 +1261,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     if (h_type == RT_MODEL_SPHERE) {   // hitting.glsl:40-42 + compute.glsl:199-204
         const float4* sp = reinterpret_cast<const float4*>(P.spheres + h_idx);
         float4 A, B, C;
-        if (P.sph_mat_lds >= 0) {   // the shading tables: the whole record from LDS
+        if (STD || P.sph_mat_lds >= 0) {   // the shading tables: the whole record from LDS
             A = rt_dyn_lds[P.sph_lds + 2 * h_idx];
             B = rt_dyn_lds[P.sph_lds + 2 * h_idx + 1];
             C = rt_dyn_lds[P.sph_mat_lds + h_idx];
@@ -1270,7 +1282,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         front = true;
         material = ldg_i(&P.media[h_idx].phase_material);
         tex_id = ldg_i(&P.media[h_idx].texture_id);
-    } else if (h_type == RT_MODEL_BOX && P.box_mat_lds >= 0) {
+    } else if (h_type == RT_MODEL_BOX && (STD ? PK_INLINE : P.box_mat_lds >= 0)) {
         // a compact box from the shading tables: face h_face's normal rebuilt bit for bit from the
         // compact record (canonical axis and value, the zero components' signs in c2.w), material,
         // texture and emission of quads[0] (compute.glsl:217-221)
@@ -1305,7 +1317,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     // (profiles/r05_u_lib_ab.log).
     const bool solid_tex = !PK_INLINE && ((tex_id >> 28) & 0xF) == RT_TEXTYPE_SOLID;
     float sc[3] = {0.0f, 0.0f, 0.0f};
-    if (solid_tex) texel_slot(P, (tex_id >> 12) & 7, tex_id & 0xFFF, 0, sc);
+    if (solid_tex) texel_slot<STD>(P, (tex_id >> 12) & 7, tex_id & 0xFFF, 0, sc);
     // scatter (scatter.glsl:43-98)
     int mid = (material >> 16) & 0xFFFF;
     bool skip_pdf = false, should = false;
@@ -1372,7 +1384,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
     }
     S.o = p;
     if (skip_pdf) {
-        S.acc = mul3(S.acc, solid_tex ? mk3(sc[0], sc[1], sc[2]) : texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time));
+        S.acc = mul3(S.acc, solid_tex ? mk3(sc[0], sc[1], sc[2]) : texture_color<PK_INLINE, STD>(P, p, tex_id, S.uvs, S.time));
         S.d = d;
         if (STATS) st_add(st, ST_SH_TEX_CYC, clock64() - c0);
         return false;
@@ -1402,7 +1414,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
         st_add(st, ST_SH_MIX_CYC, c1 - c0);
         c0 = c1;
     }
-    v3 att = solid_tex ? mk3(sc[0], sc[1], sc[2]) : texture_color<PK_INLINE>(P, p, tex_id, S.uvs, S.time);
+    v3 att = solid_tex ? mk3(sc[0], sc[1], sc[2]) : texture_color<PK_INLINE, STD>(P, p, tex_id, S.uvs, S.time);
     if (STATS) st_add(st, ST_SH_TEX_CYC, clock64() - c0);
     S.acc = mul3(S.acc, divs3(scale3(att, spdf), pdf));
     S.d = d;
@@ -1411,7 +1423,7 @@ __device__ __forceinline__ bool shade(const KP& P, Path& S, const Hit& h, float 
 
 // The rest of ray_color's loop body after the walk (compute.glsl:308-340): the
 // uv the walk left (compute.glsl:62), the background on a miss, else shade().
-template <bool PK_INLINE = false, bool STATS = false>
+template <bool PK_INLINE = false, bool STATS = false, bool STD = false>
 __device__ __forceinline__ bool after_trace(const KP& P, Path& S, const Hit& h, bool hit, float px, float py,
                                             v3& result, unsigned long long* st = nullptr) {
     if (h.uv_kind_idx != 0) {
@@ -1426,7 +1438,7 @@ __device__ __forceinline__ bool after_trace(const KP& P, Path& S, const Hit& h, 
         result = mul3(S.acc, mk3(P.background[0], P.background[1], P.background[2]));
         return true;
     }
-    return shade<PK_INLINE, STATS>(P, S, h, px, py, result, st);
+    return shade<PK_INLINE, STATS, STD>(P, S, h, px, py, result, st);
 }
 
 // Camera ray of frame `frame_count` (compute.glsl:345-350, random.glsl:19-30,82-100).

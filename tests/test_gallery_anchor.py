@@ -173,7 +173,15 @@ def test_scene0_sky_through_the_kernel(gpu, scene0_top):
 # profiles/r03_gallery_spp_probe.log), the depth, nor light sampling (registering the
 # light quad moves earth to 1.52, profiles/r03_gallery_light_probe.log) accounts for
 # (DESIGN.md §2).
-GPU_REGION_TOL = {"glass": 0.24, "metal": 0.11, "blue_fog": 0.04, "earth": 0.07, "perlin": 0.04}
+# Round 6: the metal offset is attributed -- the book's earlier metal scatter,
+# reflect(unit(dir)) + fuzz * random_in_unit_sphere, instead of the reference sources' normalised
+# reflection + fuzz * random_unit_vector (scatter.glsl:12-15), moves the metal region by x1.049-1.051
+# and nothing else (tools/scene8_residual_probe.py --r6, profiles/r06_scene8_residual_probe.log:
+# 0.942 -> 0.988 of the gallery): the gallery was rendered with that form.  So the product's metal
+# region is expected at 1 / 1.049 = 0.953 of the gallery, within the seed data's spread about it
+# (0.940-0.956, sd 0.015) + 3 sd: 6% (was 11% about 1.0).  Earth stays unattributed.
+GPU_REGION_CENTRE = {"glass": 1.0, "metal": 0.953, "blue_fog": 1.0, "earth": 1.0, "perlin": 1.0}
+GPU_REGION_TOL = {"glass": 0.24, "metal": 0.06, "blue_fog": 0.04, "earth": 0.07, "perlin": 0.04}
 LIN_RAW_TOL = 0.08   # every region, raw floats in the linear domain (round 2's single bound)
 
 
@@ -212,8 +220,8 @@ def test_scene8_regions_match_gallery_full_size_gpu(gpu, bvh):
         ratio = lin_png[regs[name]].mean(0) / np.array(fx[name]["lin_mean"])
         report[name] = np.round(ratio, 3).tolist()
     print(f"scene 8 ({bvh} BVH), 800x600, 4096 spp, depth 6, region mean / gallery (PNG pipeline):", report)
-    bad = {k: v for k, v in report.items() if max(abs(x - 1.0) for x in v) > GPU_REGION_TOL[k]}
-    assert not bad, f"region mean ratio outside GPU_REGION_TOL: {bad} (all: {report})"
+    bad = {k: v for k, v in report.items() if max(abs(x - GPU_REGION_CENTRE[k]) for x in v) > GPU_REGION_TOL[k]}
+    assert not bad, f"region mean ratio outside GPU_REGION_CENTRE +- GPU_REGION_TOL: {bad} (all: {report})"
     # The linear-domain bound kept beside the per-region PNG tolerances: the raw
     # floats, clipped to [0, 1], of every region -- glass included -- within 8% of the gallery's
     # linearised means.  This render is seed 1's, bit-exact by the rest of the suite; measured

@@ -34,7 +34,8 @@ def main():
         tpl = re.search(r"ILb(\d)ELi(\d)ELb(\d)ELb(\d)ELi(\d+)ELb(\d)ELi(\d+)E", r["name"])
         tag = ("LINK=%s MINW=%s STATS=%s LDSN=%s BLOCK=%s FAST=%s OPT=%s" % tpl.groups()) if tpl else r["name"]
         print(f"{tag:60s} VGPR {r.get('VGPRs', '?'):>4} AGPR {r.get('AGPRs', '?'):>3} "
-              f"spillV {r.get('VGPRs Spill', '?'):>3} scratch {r.get('ScratchSize [bytes/lane]', '?'):>4} "
+              f"spillV {r.get('VGPRs Spill', '?'):>3} spillS {r.get('SGPRs Spill', '?'):>3} "
+              f"scratch {r.get('ScratchSize [bytes/lane]', '?'):>4} "
               f"occ {r.get('Occupancy [waves/SIMD]', '?')}")
 
 

@@ -15,6 +15,7 @@ unchanged):
 Each renders scene 8 at W x H, depth 6 (the gallery's, profiles/r02_gallery_depth_probe.log),
 N spp with the same frames; the regions' linear means (raw floats clipped to [0, 1]) over the
 gallery's.  usage: python tools/scene8_residual_probe.py [W H spp] > profiles/r05_scene8_residual_probe.log
+       python tools/scene8_residual_probe.py --r6 [W H spp] > profiles/r06_scene8_residual_probe.log
 """
 import json
 import os
@@ -32,12 +33,19 @@ import rtamd  # noqa: E402
 FIX = json.load(open(os.path.join(REPO, "tests", "golden", "gallery.json")))
 REGIONS = ("glass", "metal", "blue_fog", "earth", "perlin")
 BUILD = os.path.join(REPO, "oracle", "build")
-VARIANTS = [("shipped", "liboracle.so"), ("sin_f64", "liboracle_probe_sin.so"),
-            ("q1_keep", "liboracle_probe_q1a.so"), ("q1_fog", "liboracle_probe_q1b.so")]
+VARIANTS = [("shipped", "liboracle.so", 6), ("sin_f64", "liboracle_probe_sin.so", 6),
+            ("q1_keep", "liboracle_probe_q1a.so", 6), ("q1_fog", "liboracle_probe_q1b.so", 6)]
+# round 6 (--r6): the gallery's depth on the metal region alone, and the metal
+# scatter's fuzz forms -- reflect(unit(dir)) + fuzz * random_in_unit_sphere (the book's earlier
+# form), and the reflected direction left unnormalised
+VARIANTS_R6 = [("shipped", "liboracle.so", 6), ("depth5", "liboracle.so", 5),
+               ("metal_ball", "liboracle_probe_metal1.so", 6), ("metal_raw", "liboracle_probe_metal2.so", 6)]
 
 
 def main():
-    W, H, spp = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (400, 300, 256)))
+    r6 = "--r6" in sys.argv
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    W, H, spp = (int(x) for x in (args[:3] if len(args) > 2 else (400, 300, 256)))
     os.system(f"make -s -C {os.path.join(REPO, 'oracle')} all probe")
     sc = rtamd.Scene(8, W, H, seed=1)
     regs = gr.scene8_regions(sc.camera, W, H, erode=1)
@@ -47,10 +55,10 @@ def main():
           f"gallery's linearised mean, per channel; px per region: "
           f"{ {n: int(regs[n].sum()) for n in REGIONS} }", flush=True)
     base = None
-    for name, lib in VARIANTS:
+    for name, lib, depth in (VARIANTS_R6 if r6 else VARIANTS):
         pyoracle.LIB, pyoracle._L = os.path.join(BUILD, lib), None
         t = time.time()
-        img = pyoracle.render(pyoracle.OracleScene(sc, max_depth=6, spp=spp), rf, nthreads=os.cpu_count())
+        img = pyoracle.render(pyoracle.OracleScene(sc, max_depth=depth, spp=spp), rf, nthreads=os.cpu_count())
         lin = np.clip(np.nan_to_num(img[..., :3].astype(np.float64), nan=0.0), 0.0, 1.0)
         ratio = {n: lin[regs[n]].mean(0) / np.array(fx[n]["lin_mean"]) for n in REGIONS}
         if base is None:
