@@ -551,11 +551,49 @@ def main():
         except Exception as e:  # the baseline is reported, not required
             log("cpu baseline failed:", repr(e))
     extra["cpu_baseline"] = cpu
+    if world == 1:
+        try:
+            extra["camera_move_host_ms"] = camera_move_cost(ctx, scene, factors)
+        except Exception as e:  # noqa: BLE001 -- reported, not required
+            log("camera move cost failed:", repr(e))
     guard.emit(extra)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
     guard.close()
+
+
+def camera_move_cost(ctx, scene, factors, reps=5):
+    """Host time a camera move adds to the next rt_render, after the timed region: the
+    walk's node collapse is planned for the camera (rt_capi.hip plan_collapse, a grid of camera rays
+    walked on the host, then the links rebuilt and re-uploaded), so an interactive host pays it on
+    every move.  Median host time of a one-frame rt_render after a small translation of the camera,
+    minus the same call with the camera unchanged (both enqueue only; the device work is not
+    waited for).  Any plan is exact, so the image does not depend on it."""
+    import torch
+    cam = np.array(scene.camera, np.float32).copy()
+    def call(moved, k):
+        c = cam.copy()
+        if moved:
+            d = np.float32(0.01 * (k + 1))
+            c[4:7] += d    # camera_pos (rt_camera_ubo)
+            c[8:11] += d   # up_left: the same view, translated
+        ctx.set_camera(c)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        ctx.render(1, factors[:1])
+        dt = time.perf_counter() - t
+        torch.cuda.synchronize()
+        return dt
+    call(False, 0)
+    still = [call(False, 0) for _ in range(reps)]
+    moved = [call(True, k) for k in range(reps)]
+    ctx.set_camera(cam)
+    return {"move_ms": round((float(np.median(moved)) - float(np.median(still))) * 1e3, 3),
+            "render_call_still_ms": round(float(np.median(still)) * 1e3, 3),
+            "render_call_moved_ms": round(float(np.median(moved)) * 1e3, 3),
+            "what": "host time of a one-frame rt_render after a camera translation minus with the camera "
+                    "unchanged (the collapse re-plan and link upload; bench.py camera_move_cost)"}
 
 
 def finish(args, scene, ctx, image, rank, world, dev, factors, n_frames):
