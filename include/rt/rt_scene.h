@@ -40,7 +40,8 @@ typedef struct rts_info {
 } rts_info;
 
 /* Build scene `scene_id` (0..9) for a width x height image.  asset_dir holds
- * earthmap.ppm (scenes 2 and 8); NULL = "<repo>/assets" resolved at build time.
+ * earthmap.jpg (scenes 2 and 8; the reference's textures/earthmap.jpg, decoded by
+ * rts_decode_image); NULL = "<repo>/assets" resolved at build time.
  * Returns 0 or a negative rt.h error code. */
 int rts_build(int scene_id, int width, int height, uint64_t seed,
               const char* asset_dir, rts_scene** out);
@@ -102,6 +103,18 @@ void rts_spp_uniforms(int spp, float* sqrt_spp, float* recip_sqrt_spp);
  * -> (byte)(pow(b/255, 1/2.2)*255) -> RGB PNG.  rgb8_out (W*H*3) optional. */
 int rts_tonemap_rgb8(const float* rgba, int width, int height, uint8_t* rgb8_out);
 int rts_save_png(const float* rgba, int width, int height, const char* path);
+
+/* ImageTexture.create's read (ImageTexture.java:22-85: ImageIO.read, then getRGB per
+ * pixel): decode a JPEG (baseline / progressive, the IJG decoder's islow IDCT, fancy
+ * upsampling and YCbCr tables), PNG (8-bit RGB / RGBA / palette) or P6 PPM file into
+ * 8-bit R, G, B (, A) rows, row 0 = top (before ImageTexture's flip and shift).
+ * *channels = 3 or 4 (BufferedImage's colour-model components); greyscale and other
+ * component counts fail like the reference ("Unsupported image format").  pixels may be
+ * NULL (size query); else it must hold width * height * channels bytes (capacity).
+ * Message of a failure: rts_decode_last_error. */
+int rts_decode_image(const char* path, int* width, int* height, int* channels, uint8_t* pixels,
+                     size_t capacity);
+const char* rts_decode_last_error(void);
 
 /* java.util.Random known-answer hooks (tests). */
 int32_t rts_java_random_next_int(int64_t seed, int n_calls_before);

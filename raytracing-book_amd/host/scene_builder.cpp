@@ -16,6 +16,10 @@
 #include <string>
 #include <vector>
 
+namespace rts_detail {   // image_decode.cpp
+int decode_image_file(const char* path, int* w, int* h, int* comps, std::vector<uint8_t>* px);
+}
+
 #ifndef RT_ASSET_DIR
 #define RT_ASSET_DIR "assets"
 #endif
@@ -202,32 +206,25 @@ struct World {
         // PerlinNoiseTexture.getDetail = scale/100 (float)
         return tex_value_f(RT_TEXTYPE_PERLIN, idx, scale / 100.0f);
     }
-    // ImageTexture.create (ImageTexture.java:22-92) from a decoded PPM asset
+    // ImageTexture.create (ImageTexture.java:22-92): the file decoded as ImageIO + getRGB do it
+    // (image_decode.cpp), then the loop's vertical flip and wrap shift.  A name without a '/'
+    // A relative name is a resource of the asset directory (the reference's classpath
+    // "textures/"), an absolute one a file; 3 components upload as GL_RGB, 4 as GL_RGBA.
     int image_create(const char* name, int shift_x, int shift_y) {
-        std::string path = asset_dir + "/" + name;
-        FILE* fp = std::fopen(path.c_str(), "rb");
-        if (!fp) throw std::runtime_error("Failed to load image: " + path);
-        char magic[3] = {0};
-        int w = 0, h = 0, maxv = 0;
-        if (std::fscanf(fp, "%2s %d %d %d", magic, &w, &h, &maxv) != 4 || std::strcmp(magic, "P6") || maxv != 255) {
-            std::fclose(fp);
-            throw std::runtime_error("Unsupported image format: " + path);
-        }
-        std::fgetc(fp);
-        std::vector<uint8_t> src((size_t)w * h * 3);
-        size_t got = std::fread(src.data(), 1, src.size(), fp);
-        std::fclose(fp);
-        if (got != src.size()) throw std::runtime_error("Truncated image: " + path);
+        std::string path = name[0] == '/' ? std::string(name) : asset_dir + "/" + name;
+        int w = 0, h = 0, comps = 0;
+        std::vector<uint8_t> src;
+        rts_detail::decode_image_file(path.c_str(), &w, &h, &comps, &src);
         TexSlot t;
-        t.kind = RT_TEXTYPE_IMAGE; t.format = RT_TEX_RGB8; t.w = w; t.h = h;
+        t.kind = RT_TEXTYPE_IMAGE; t.format = comps == 4 ? RT_TEX_RGBA8 : RT_TEX_RGB8; t.w = w; t.h = h;
         t.bytes.resize(src.size());
         for (int y = 0; y < h; y++) {
             int sy = (h - 1 - (y - shift_y + h) % h);   // vertical flip + wrap shift
             for (int x = 0; x < w; x++) {
                 int sx = (x - shift_x + w) % w;
-                const uint8_t* p = &src[((size_t)sy * w + sx) * 3];
-                uint8_t* q = &t.bytes[((size_t)y * w + x) * 3];
-                q[0] = p[0]; q[1] = p[1]; q[2] = p[2];
+                const uint8_t* p = &src[((size_t)sy * w + sx) * comps];
+                uint8_t* q = &t.bytes[((size_t)y * w + x) * comps];
+                for (int k = 0; k < comps; k++) q[k] = p[k];
             }
         }
         textures.push_back(std::move(t));
@@ -529,7 +526,7 @@ static void scene_checker_spheres(World& W) {
 
 // Scene.java:126-139
 static void scene_earth(World& W) {
-    int earth = W.image_create("earthmap.ppm", 0, 0);
+    int earth = W.image_create("earthmap.jpg", 0, 0);
     W.add_model(W.sphere(Vec3f(0, 0, 0), 2, W.lambertian(earth)));
     W.vfov = 20; W.look_from = Vec3f(0, 0, 12); W.look_at = Vec3f(0, 0, 0);
     W.defocus_angle = 0; W.background = Vec3f(0.70f, 0.80f, 1.00f);
@@ -657,7 +654,7 @@ static void scene_final(World& W) {
     boundary = W.sphere(Vec3f(0, 0, 0), 5000, W.dielectric(1.5f));
     Material iso2 = W.isotropic(W.solid_register(1, 1, 1));
     W.add_model(W.constant_medium(boundary, 0.0001f, iso2));
-    Material earth = W.lambertian(W.image_create("earthmap.ppm", 100, 0));
+    Material earth = W.lambertian(W.image_create("earthmap.jpg", 100, 0));
     W.add_model(W.sphere(Vec3f(400, 200, 400), 100, earth));
     Material noise = W.lambertian(W.perlin_create(0.2f));
     W.add_model(W.sphere(Vec3f(220, 280, 300), 80, noise));

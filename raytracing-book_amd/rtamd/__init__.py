@@ -10,4 +10,4 @@ from ._lib import RTError, amd, amd_ab, scene_lib  # noqa: F401
 from .render import (OPTIONS, RaytraceExecutor, RenderContext, comm_unique_id, deinterleave,  # noqa: F401
                      frame_rand_factors,
                      local_rows, padded_local_rows, sah_bvh, stripe_rows_of)
-from .scene import SCENE_NAMES, Scene, SceneBuilder, save_png, spp_uniforms, tonemap_rgb8  # noqa: F401
+from .scene import SCENE_NAMES, Scene, SceneBuilder, decode_image, save_png, spp_uniforms, tonemap_rgb8  # noqa: F401

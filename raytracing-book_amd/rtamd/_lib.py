@@ -178,6 +178,9 @@ def scene_lib():
         _proto(L, "rts_build", i, i, i, i, ctypes.c_uint64, ctypes.c_char_p, ctypes.POINTER(vp))
         _proto(L, "rts_free", None, vp)
         _proto(L, "rts_last_error", ctypes.c_char_p)
+        _proto(L, "rts_decode_image", i, ctypes.c_char_p, c_int_p, c_int_p, c_int_p,
+               ctypes.POINTER(ctypes.c_uint8), sz)
+        _proto(L, "rts_decode_last_error", ctypes.c_char_p)
         _proto(L, "rts_get_info", i, vp, ctypes.POINTER(RtsInfo))
         _proto(L, "rts_get_buffer", i, vp, i, ctypes.POINTER(vp), ctypes.POINTER(sz))
         _proto(L, "rts_get_texture", i, vp, i, c_int_p, c_int_p, c_int_p, ctypes.POINTER(vp), ctypes.POINTER(sz))

@@ -131,6 +131,22 @@ def save_png(rgba, path):
         raise IOError(f"saving {path} failed ({rc})")
 
 
+def decode_image(path):
+    """ImageTexture.create's read (ImageTexture.java:22-85: ImageIO.read + getRGB) of a JPEG,
+    PNG or P6 PPM file -> uint8 [H, W, 3 or 4], row 0 = top (rt_scene.h rts_decode_image).
+    Raises ValueError where the reference throws (unsupported component counts)."""
+    L = _lib.scene_lib()
+    w, h, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    p = str(path).encode()
+    if L.rts_decode_image(p, ctypes.byref(w), ctypes.byref(h), ctypes.byref(c), None, 0):
+        raise ValueError(L.rts_decode_last_error().decode())
+    out = np.empty((h.value, w.value, c.value), dtype=np.uint8)
+    if L.rts_decode_image(p, ctypes.byref(w), ctypes.byref(h), ctypes.byref(c),
+                          out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), out.size):
+        raise ValueError(L.rts_decode_last_error().decode())
+    return out
+
+
 MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_DIFFUSE_LIGHT, MAT_ISOTROPIC = range(5)
 
 

@@ -1,0 +1,141 @@
+"""ImageTexture.create's image read (ImageTexture.java:22-85: ImageIO.read, getRGB per pixel,
+then the vertical flip and wrap shift) through rt_scene.h rts_decode_image / the scene builder.
+
+Pins:
+* the reference's own texture, textures/earthmap.jpg (committed as assets/earthmap.jpg), decodes
+  to assets/earthmap.ppm byte for byte -- the libjpeg(-turbo) decode of it (tools/make_assets.py),
+  i.e. the IJG decoder javax.imageio wraps, with its default islow IDCT;
+* seeded JPEGs (baseline and progressive; 4:4:4, 4:2:2 and 4:2:0; restart intervals) and PNGs
+  (RGB, RGBA, palettes of 1/4/8 bits with and without tRNS) against Pillow's decode, byte for
+  byte, when Pillow is importable (it is in this image);
+* the reference's error behaviour: images with other than 3 or 4 colour components are refused.
+"""
+import io
+import os
+
+import numpy as np
+import pytest
+
+import rtamd
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ASSETS = os.path.join(REPO, "assets")
+
+
+def read_ppm(path):
+    data = open(path, "rb").read()
+    parts = data.split(maxsplit=4)
+    w, h = int(parts[1]), int(parts[2])
+    return np.frombuffer(data[-w * h * 3:], np.uint8).reshape(h, w, 3)
+
+
+def test_earthmap_jpg_decodes_to_the_committed_pin():
+    img = rtamd.decode_image(os.path.join(ASSETS, "earthmap.jpg"))
+    assert img.shape == (512, 1024, 3)
+    assert np.array_equal(img, read_ppm(os.path.join(ASSETS, "earthmap.ppm")))
+
+
+def test_scene8_uploads_imagetexture_loop_of_the_decoded_jpg():
+    """ImageTexture.create("textures/earthmap.jpg", 100, 0) (Scene.java): row y of the texture is
+    source row H-1-((y - 0 + H) % H), column x is source column (x - 100 + W) % W."""
+    src = rtamd.decode_image(os.path.join(ASSETS, "earthmap.jpg"))
+    sc = rtamd.Scene(8, 64, 36)
+    tex = [t for t in sc.textures if (t.width, t.height) == (1024, 512)]
+    assert len(tex) == 1 and tex[0].format == rtamd.scene.TEX_RGB8
+    got = np.frombuffer(bytes(tex[0].data), np.uint8).reshape(512, 1024, 3)
+    want = np.roll(src[::-1], 100, axis=1)
+    assert np.array_equal(got, want)
+
+
+def _roundtrip(tmp_path, name, data):
+    p = tmp_path / name
+    p.write_bytes(data)
+    return str(p)
+
+
+@pytest.mark.parametrize("subsampling", [0, 1, 2])
+@pytest.mark.parametrize("progressive", [False, True])
+def test_jpeg_matches_libjpeg(tmp_path, subsampling, progressive):
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(100 + subsampling + 3 * progressive)
+    for trial in range(12):
+        w, h = int(rng.integers(1, 70)), int(rng.integers(1, 50))
+        if trial % 2:
+            arr = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        else:
+            yy, xx = np.mgrid[0:h, 0:w]
+            arr = ((np.stack([xx * 3, yy * 5, xx + yy], -1) + rng.integers(0, 40, (h, w, 3))) % 256).astype(np.uint8)
+        kw = {}
+        if trial % 3 == 0:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 5))
+        buf = io.BytesIO()
+        Image.fromarray(arr).save(buf, "JPEG", quality=int(rng.integers(20, 96)), subsampling=subsampling,
+                                  progressive=progressive, **kw)
+        path = _roundtrip(tmp_path, "t.jpg", buf.getvalue())
+        want = np.asarray(Image.open(path).convert("RGB"))
+        got = rtamd.decode_image(path)
+        assert np.array_equal(got, want), (w, h, trial)
+
+
+@pytest.mark.parametrize("mode", ["RGB", "RGBA", "P8", "P4", "P1", "P8T"])
+def test_png_matches_pillow(tmp_path, mode):
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        w, h = int(rng.integers(1, 60)), int(rng.integers(1, 40))
+        arr = rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+        buf = io.BytesIO()
+        if mode in ("RGB", "RGBA"):
+            Image.fromarray(arr[..., :len(mode)], mode).save(buf, "PNG", optimize=bool(trial % 2))
+            conv = mode
+        else:
+            ncol = {"P8": 256, "P4": 16, "P1": 2, "P8T": 20}[mode]
+            im = Image.fromarray(arr[..., :3]).quantize(ncol)
+            if mode == "P8T":
+                im.save(buf, "PNG", transparency=bytes(rng.integers(0, 256, ncol, dtype=np.uint8)))
+                conv = "RGBA"
+            else:
+                im.save(buf, "PNG", bits={"P8": 8, "P4": 4, "P1": 1}[mode])
+                conv = "RGB"
+        path = _roundtrip(tmp_path, "t.png", buf.getvalue())
+        want = np.asarray(Image.open(path).convert(conv))
+        assert np.array_equal(rtamd.decode_image(path), want)
+
+
+def test_components_other_than_3_or_4_are_refused(tmp_path):
+    """ImageTexture.java:41-49: "Unsupported image format" unless 3 or 4 components."""
+    Image = pytest.importorskip("PIL.Image")
+    g = np.arange(48, dtype=np.uint8).reshape(6, 8)
+    for fmt, im in (("JPEG", Image.fromarray(g, "L")), ("PNG", Image.fromarray(g, "L")),
+                    ("PNG", Image.fromarray(np.stack([g, g], -1), "LA"))):
+        buf = io.BytesIO()
+        im.save(buf, fmt)
+        path = _roundtrip(tmp_path, "g." + fmt.lower(), buf.getvalue())
+        with pytest.raises(ValueError, match="Unsupported image format"):
+            rtamd.decode_image(path)
+    with pytest.raises(ValueError, match="Failed to load image"):
+        rtamd.decode_image(str(tmp_path / "missing.jpg"))
+
+
+def test_custom_scene_takes_an_rgba_png_texture(tmp_path):
+    """A custom scene's ImageTexture.create(path, sx, sy) of a 4-component image uploads GL_RGBA
+    bytes in the flipped, shifted order."""
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(3)
+    arr = rng.integers(0, 256, (9, 13, 4), dtype=np.uint8)
+    path = tmp_path / "tex.png"
+    Image.fromarray(arr, "RGBA").save(path)
+    b = rtamd.SceneBuilder(seed=1)
+    tex = b.image(str(path), 5, 2)
+    b.add(b.sphere((0, 0, -1), 0.5, b.lambertian(tex)))
+    b.camera(look_from=(0, 0, 1), look_at=(0, 0, -1))
+    sc = b.finish(16, 9)
+    t = [t for t in sc.textures if (t.width, t.height) == (13, 9)]
+    assert len(t) == 1 and t[0].format == rtamd.scene.TEX_RGBA8
+    got = np.frombuffer(bytes(t[0].data), np.uint8).reshape(9, 13, 4)
+    want = np.empty_like(arr)
+    for y in range(9):
+        sy = 9 - 1 - (y - 2 + 9) % 9
+        for x in range(13):
+            want[y, x] = arr[sy, (x - 5 + 13) % 13]
+    assert np.array_equal(got, want)

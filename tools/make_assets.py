@@ -1,11 +1,11 @@
 """Decode the reference's texture asset into a dependency-free PPM.
 
 The reference loads src/main/resources/textures/earthmap.jpg through
-javax.imageio (ImageTexture.java:22-92).  /root/reference is absent on the GPU
-box and the C++ scene builder has no JPEG decoder, so the decoded RGB8 pixels
-(top row first, unshifted; ImageTexture's flip/shift is applied by the builder)
-are committed as assets/earthmap.ppm.  Decoder: Pillow's libjpeg; Java ImageIO's
-IDCT may differ by +-1 per channel (texture bits are not pinned by any test).
+javax.imageio (ImageTexture.java:22-92).  Since round 6 the scene builder decodes
+assets/earthmap.jpg itself (host/image_decode.cpp, the IJG decoder's islow IDCT,
+fancy upsampling and YCbCr tables); this script's output, assets/earthmap.ppm
+(Pillow's libjpeg-turbo decode, top row first, unshifted), is the pin that decode
+is checked against byte for byte (tests/test_image_decode.py).
 Run in the dev container: python tools/make_assets.py
 """
 import os
