@@ -1151,6 +1151,9 @@ __device__ __forceinline__ v3 rand_unit_vec(float& rf, float px, float py) {
         float y = -1.0f + rnd(rf, px, py) * 2.0f;
         float z = -1.0f + rnd(rf, px, py) * 2.0f;
         p = mk3(x, y, z);
+#ifdef RT_ABL_UNITVEC1   // ablation (A/B builds only, not exact): the first candidate, no rejection
+        break;
+#endif
         if (g_dot(p, p) < 1.0f) break;
     }
     return g_normalize(p);
