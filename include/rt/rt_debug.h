@@ -150,6 +150,10 @@ enum {
                                            leaves, order and ray_t; rt_capi.hip
                                            rebuild_inner): 1 greedy surface-area splits,
                                            2 the least summed inner-box area (default); 0 off */
+    RT_OPTION_TAIL_CHUNKS = 27,         /* staged launches end with this many one-frame
+                                           chunks: the units claimed last are short (only
+                                           the grouping of samples into units changes);
+                                           -1 (default): 1 above 1024 BVH nodes, else 0  */
     RT_OPTION_KERNEL_VARIANT = 100,     /* A/B build: 0, 37, 30, 61 (+ stats twins)         */
     RT_OPTION_DEBUG_FLAGS = 101         /* A/B build: ablations, NOT exact                  */
 };

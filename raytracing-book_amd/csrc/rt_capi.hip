@@ -202,6 +202,8 @@ struct rt_ctx {
     // (scene 8 -5% against ordered chunks).
     int chunk_target = 16;          // ordered chunks (RT_CHUNK_TARGET)
     int staged_chunk_target = 48;   // staged chunks (RT_STAGED_CHUNK_TARGET)
+    int tail_chunks = -1;           // option tail_chunks: staged launches end with this many one-frame chunks
+                                    // (-1: tail_chunks_for the tree)
     int stage_tiles = 1 << 20;      // in effect always staged (the measured best with render_stream)
     bool fastdiv = true;   // shared-reciprocal divisions where exact (env RT_FASTDIV=0 disables; A/B)
     bool box_pretest = true;   // the canonical box tests' bounds pre-test (env RT_BOX_PRETEST=0 disables; A/B)
@@ -764,6 +766,14 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
 // Rounds only regroup which lanes walk and
 // test leaves together: every lane's node and prim sequence is unchanged (bit-identical).
 int walk_frac_for(int n_nodes) { return n_nodes <= RT_SMALL_TREE ? 8 : n_nodes <= 1024 ? 32 : 48; }
+
+// The default number of one-frame chunks that end a staged launch (option tail_chunks -1): the units
+// the grid claims last are then 64 samples, so its waves finish closer together.  Measured (round 6,
+// profiles/r06_l_opts_s*.log, r06_m_opts_s*.log): scene 8 (1793 nodes) -0.9% with one (+0.6% with 4,
+// +3.5% with 8: a short unit's claim and set-up cost more than the imbalance), scene 0 (511 nodes)
+// +0.4%, scene 6 +0.2%; so one above 1024 nodes, none otherwise.  Only the grouping of samples into
+// units changes (bit-identical; tests/test_gpu_fullsize.py gates 0 and 7 at 1080p).
+int tail_chunks_for(int n_nodes) { return n_nodes > 1024 ? 1 : 0; }
 
 // The spine of the link-format walk (rt_kernel.hip spine_entry): every walk starts at the
 // root and, while it hits, goes on to the right child (compute.glsl:259-260), so its first
@@ -2470,6 +2480,17 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             a.n_chunks = (nf + a.chunk_frames - 1) / a.chunk_frames;
             if (a.n_chunks == 1) a.samples = nullptr;   // one chunk: the running mean in place
             else if (staged) a.samples = (float4*)d.samples.ptr;
+            // staged: the last frames as one-frame chunks (the units claimed last are then short,
+            // so the grid's waves finish close together); the chunks before keep their size
+            a.tail_chunks = 0;
+            const int tail = c->tail_chunks >= 0 ? c->tail_chunks : tail_chunks_for(c->n_link_nodes);
+            if (a.samples && tail > 0 && a.n_chunks > 1 && (c->variant == 0 || c->variant == 39)) {
+                const int tc = std::min(tail, nf - 1);
+                const int nm = nf - tc;
+                const int cm = (nm + a.chunk_frames - 1) / a.chunk_frames;
+                a.n_chunks = cm + tc;
+                a.tail_chunks = tc;
+            }
             // Sparse staging (render_stream): most samples' colours are exactly zero (scene 8: 96%:
             // a path that ends without reaching the light), so each sample writes a flag byte and
             // only the others their 16-byte colour; fold_kernel reads a clear flag as the zero
@@ -2946,6 +2967,7 @@ int rt_debug_set_option(rt_ctx* c, int option, int v) {
         case RT_OPTION_WATCHDOG_MS: if (v < 0) return bad(); c->watchdog_ticks = (unsigned long long)v * 100000ull; break;
         case RT_OPTION_CHUNK_WAIT_MS: if (v < 0) return bad(); c->chunk_wait_ticks = (unsigned long long)v * 100000ull; break;
         case RT_OPTION_LDS_NODE_CAP: if (v < 0) return bad(); c->lds_node_cap = v; break;
+        case RT_OPTION_TAIL_CHUNKS: if (v < -1 || v > RT_MAX_FRAMES_PER_LAUNCH) return bad(); c->tail_chunks = v; break;
 #ifdef RT_AB_KNOBS
         case RT_OPTION_KERNEL_VARIANT:
             if (!(v == 0 || v == 30 || v == 31 || v == 37 || v == 38 || v == 39 || v == 61 || v == 69)) return bad();
@@ -2987,6 +3009,7 @@ int rt_debug_get_option(rt_ctx* c, int option, int* v) {
         case RT_OPTION_WATCHDOG_MS: *v = (int)std::min<unsigned long long>(INT_MAX, c->watchdog_ticks / 100000ull); break;
         case RT_OPTION_CHUNK_WAIT_MS: *v = (int)std::min<unsigned long long>(INT_MAX, c->chunk_wait_ticks / 100000ull); break;
         case RT_OPTION_LDS_NODE_CAP: *v = c->lds_node_cap; break;
+        case RT_OPTION_TAIL_CHUNKS: *v = c->tail_chunks; break;
 #ifdef RT_AB_KNOBS
         case RT_OPTION_KERNEL_VARIANT: *v = c->variant; break;
         case RT_OPTION_DEBUG_FLAGS: *v = c->debug_flags; break;

@@ -119,8 +119,10 @@ struct rt_kernel_args {
                                  // record count, then census_cap records of RT_CENSUS_WORDS words per wave
     int census_cap, census_waves;
     int* tile_counter;           // persistent kernel: next work unit (zeroed per launch)
-    // work split: unit = chunk * n_tiles + tile, chunk = frames [c*chunk_frames, ...) (ordered chunks)
-    int n_chunks, chunk_frames;
+    // work split: unit = chunk * n_tiles + tile, chunk = frames [c*chunk_frames, ...) (ordered chunks);
+    // staged launches may end with tail_chunks chunks of one frame each (option tail_chunks): chunk
+    // c >= n_chunks - tail_chunks holds frame n_frames - (n_chunks - c)
+    int n_chunks, chunk_frames, tail_chunks;
     unsigned* tile_done;         // ordered chunks: per tile, the chunks published so far (zeroed per launch)
     float4* samples;             // staged chunks: per-frame colours [n_frames][n_pixels]; nullptr = ordered / one chunk
     uint8_t* sflags;             // sparse staging (render_stream): per sample [n_frames][n_pixels] 1 when its colour

@@ -69,8 +69,16 @@ __device__ __forceinline__ UnitGeo unit_geo(const KP& P, int u, int n_tiles, int
     g.ly0 = (g.tile / tiles_x) * 8;
     g.wt = min(8, P.width - g.tx0);
     g.ht = min(8, P.local_rows - g.ly0);
-    g.f0 = g.chunk * P.chunk_frames;
-    g.f1 = min(P.n_frames, g.f0 + P.chunk_frames);
+    // the grid's last units are the tail chunks' (units are claimed chunk by chunk): one frame each,
+    // so waves finish within a short unit of each other
+    const int c_main = P.n_chunks - P.tail_chunks;
+    if (g.chunk < c_main) {
+        g.f0 = g.chunk * P.chunk_frames;
+        g.f1 = min(P.n_frames - P.tail_chunks, g.f0 + P.chunk_frames);
+    } else {
+        g.f0 = P.n_frames - (P.n_chunks - g.chunk);
+        g.f1 = g.f0 + 1;
+    }
     g.total = (uint32_t)(g.wt * g.ht * (g.f1 - g.f0));
     return g;
 }

@@ -100,7 +100,7 @@ def deinterleave(gathered, height, world, stripe_rows):
 OPTIONS = {"box_pretest": 1, "fastdiv": 2, "sph_lds": 3, "big_wg": 4, "chunk_target": 5,
            "staged_chunk_target": 6, "stage_tiles": 7, "sm_batch": 8, "sm_frac": 9, "walk_frac": 10,
            "watchdog_ms": 11, "chunk_wait_ms": 12, "lds_node_cap": 13, "compact_boxes": 14, "spine": 15,
-           "tl_leaf_lds": 16, "perlin_packed": 17, "sparse_stage": 18, "sphere_pairs": 19, "leaf_prefetch": 20, "tl_small_lds": 21, "shade_lds": 22, "box_vnodes": 23, "zero_dir_end": 24, "collapse": 25, "rebuild": 26, "kernel_variant": 100, "debug_flags": 101}
+           "tl_leaf_lds": 16, "perlin_packed": 17, "sparse_stage": 18, "sphere_pairs": 19, "leaf_prefetch": 20, "tl_small_lds": 21, "shade_lds": 22, "box_vnodes": 23, "zero_dir_end": 24, "collapse": 25, "rebuild": 26, "tail_chunks": 27, "kernel_variant": 100, "debug_flags": 101}
 # rt_debug_last_launch fields
 LAUNCH_FIELDS = ("shape", "block", "fastdiv", "pretest", "lds_bytes", "lds_nodes", "box_records", "staged",
                  "chunks", "spine", "sparse", "sphere_pairs", "leaf_prefetch", "shade_lds", "walk_frac", "bvh_mode",

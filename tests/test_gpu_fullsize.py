@@ -159,6 +159,7 @@ WALK_OPTIONS = [
     ("shade_lds", {"shade_lds": 0}), ("box_vnodes", {"box_vnodes": 0}), ("zero_dir_end", {"zero_dir_end": 0}),
     ("collapse", {"collapse": 0}), ("rebuild", {"rebuild": 0}), ("rebuild", {"rebuild": 0, "collapse": 0}),
     ("two_level", {"lds_node_cap": 16384}), ("two_level_leaf_global", {"lds_node_cap": 16384, "tl_leaf_lds": 0}),
+    ("tail_chunks", {"tail_chunks": 0}), ("tail_chunks", {"tail_chunks": 7}),
 ]
 
 
