@@ -83,6 +83,15 @@ struct rt_ctx;
 int rt_debug_enable_stats(struct rt_ctx* ctx, int enable);
 int rt_debug_read_stats(struct rt_ctx* ctx, unsigned long long* out, int n);
 int rt_debug_read_census(struct rt_ctx* ctx, unsigned int* out, size_t words, size_t* needed, int* waves, int* cap);
+/* The stats twin's node-hit count (A/B experiments on the collapse plan, tools/collapse_hits_ab.py):
+ * count_node_hits(ctx, 1) zeroes and arms it (0 frees it); read_node_hits gives, per link node of
+ * the last launch's layout, the box tests that hit, then the walks begun at the root
+ * (*n_out = nodes + 1 words; out may be NULL); set_collapse_hits plans the collapse from such counts
+ * (per node of the walk's tree, breadth-first, as read with collapse and spine off) instead of the
+ * camera grid (n = 0: the grid again). */
+int rt_debug_count_node_hits(struct rt_ctx* ctx, int on);
+int rt_debug_read_node_hits(struct rt_ctx* ctx, unsigned int* out, size_t words, size_t* n_out);
+int rt_debug_set_collapse_hits(struct rt_ctx* ctx, const unsigned int* hits, size_t n, unsigned long long walks);
 
 /* Number of visible HIP devices (0 when none). */
 int rt_debug_device_count(void);

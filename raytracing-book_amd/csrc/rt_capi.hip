@@ -90,6 +90,7 @@ struct Device {
     DevBuf args;             // rt_kernel_args slot in device memory
     DevBuf stats;            // diagnostic counters (rt_debug_enable_stats)
     DevBuf census;           // the stats twin's leaf census (rt_debug_enable_stats(ctx, 2))
+    DevBuf node_hits;        // the stats twin's node-hit count (rt_debug_count_node_hits)
     int census_cap = 0, census_waves = 0;
     DevBuf counter;          // persistent-kernel work-unit counter [0] and fault word [1]
     DevBuf tile_done;        // ordered chunks: chunks published per 8x8 tile
@@ -190,6 +191,10 @@ struct rt_ctx {
     uint64_t last_ns = 0;
     int variant = 0;   // kernel structure variant (env RT_KERNEL_VARIANT; A/B only)
     int variant_no_stats = -1;   // the variant active before rt_debug_enable_stats(c, 1), restored by (c, 0)
+    // the collapse plan from measured node hits (rt_debug_set_collapse_hits): per node of the walk's
+    // tree in its breadth-first link order, the box tests that hit, and the walks begun at the root
+    std::vector<int64_t> inj_hits;
+    int64_t inj_walks = 0;
     // Work split: aim for chunk_target work units per resident wave (env
     // RT_CHUNK_TARGET; 0 = one chunk per tile), staged_chunk_target when staged
     // (RT_STAGED_CHUNK_TARGET).  With at least stage_tiles tiles
@@ -688,6 +693,7 @@ std::vector<rt_dnode> rebuild_inner_impl(const std::vector<rt_dnode>& dn, int mo
 // counts taken by a dynamic programme over the tree; the root stays (the walk starts there).
 // tools/node_collapse_study.py: on scene 8 this grid's choice cuts the node tests of the
 // reference's own walks by 11.5% beyond the spine (the best choice for the walks themselves: 16%).
+std::vector<uint8_t> plan_from_hits(const std::vector<rt_dnode>& dn, const std::vector<int64_t>& H, int64_t walks);
 std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_camera_ubo& cam, int width, int height) {
     const size_t n = dn.size();
     std::vector<uint8_t> drop(n, 0);
@@ -727,6 +733,19 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
             }
         }
     }
+    return plan_from_hits(dn, H, (int64_t)gx * gy);
+}
+
+// The collapse's dynamic programme for given hit counts H (per node of dn) over `walks` walks
+// begun at the root (plan_collapse's grid, or counts measured on the walks themselves by the stats
+// twin, rt_debug_set_collapse_hits).
+std::vector<uint8_t> plan_from_hits(const std::vector<rt_dnode>& dn, const std::vector<int64_t>& H, int64_t walks) {
+    const size_t n = dn.size();
+    std::vector<uint8_t> drop(n, 0);
+    if (H.size() != n || n <= RT_SMALL_TREE || n > RT_LINK_MAX_NODES || !boxes_nest(dn)) return drop;
+    for (const rt_dnode& d : dn)
+        if (!(d.xmin < d.xmax && d.ymin < d.ymax && d.zmin < d.zmax)) return drop;
+    auto is_leaf = [&](size_t k) { return (dn[k].meta & 0xF0000u) != 0; };
     // cost(k, v): the fewest tests of k's subtree when k's place is reached v times
     std::map<std::pair<uint32_t, int64_t>, std::pair<int64_t, bool>> memo;
     std::function<std::pair<int64_t, bool>(uint32_t, int64_t)> cost = [&](uint32_t k, int64_t v) {
@@ -744,7 +763,7 @@ std::vector<uint8_t> plan_collapse(const std::vector<rt_dnode>& dn, const rt_cam
         memo.emplace(key, best);
         return best;
     };
-    std::vector<std::pair<uint32_t, int64_t>> st{{0u, (int64_t)gx * gy}};
+    std::vector<std::pair<uint32_t, int64_t>> st{{0u, walks}};
     while (!st.empty()) {
         const auto [k, v] = st.back();
         st.pop_back();
@@ -2166,7 +2185,23 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
             std::vector<uint8_t> drop;
             if (use_c) {
                 try {
-                    drop = plan_collapse(wdn, c->cam, c->width, c->height);
+                    if (!c->inj_hits.empty() && c->inj_hits.size() >= wdn.size()) {
+                        // measured hits, given per link node (breadth-first): back to dn's order
+                        std::vector<uint32_t> order{0u};
+                        for (size_t q = 0; q < order.size() && order.size() <= wdn.size(); q++) {
+                            const uint32_t k = order[q];
+                            if ((wdn[k].meta & 0xF0000u) != 0 || k + 1 >= wdn.size()) continue;
+                            order.push_back(k + 1);
+                            order.push_back(wdn[k + 1].meta & 0xFFFFu);
+                        }
+                        std::vector<int64_t> H(wdn.size(), 0);
+                        if (order.size() == wdn.size())
+                            for (size_t q = 0; q < order.size(); q++)
+                                if (order[q] < wdn.size()) H[order[q]] = c->inj_hits[q];
+                        drop = plan_from_hits(wdn, H, c->inj_walks);
+                    } else {
+                        drop = plan_collapse(wdn, c->cam, c->width, c->height);
+                    }
                 } catch (const std::bad_alloc&) {   // no plan: the walk keeps every node
                     drop.clear();
                 }
@@ -2395,6 +2430,7 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
         a.stats = (unsigned long long*)d.stats.ptr;
         a.census = (unsigned*)d.census.ptr;
         a.census_cap = d.census_cap;
+        a.node_hits = (unsigned*)d.node_hits.ptr;
         a.census_waves = d.census_waves;
         a.local_rows = d.local_rows;
         a.rank = d.rank;
@@ -2913,6 +2949,58 @@ int rt_debug_read_census(rt_ctx* c, unsigned* out, size_t words, size_t* needed,
     if (!n) return RT_OK;
     HIPCHK(c, hipSetDevice(d.id));
     return d2h(c, d, out, d.census.ptr, d.census.bytes);
+}
+
+// The stats twin's node-hit count (tools/collapse_hits_ab.py): on = 1 allocates and zeroes one word
+// per possible link node plus the walk count; the stats twin's launches then add to it.
+int rt_debug_count_node_hits(rt_ctx* c, int on) {
+    if (!c) return RT_ERR_INVALID_ARG;
+    for (Device& d : c->devs) {
+        HIPCHK(c, hipSetDevice(d.id));
+        HIPCHK(c, hipStreamSynchronize(d.stream));
+        if (!on) {
+            dev_free(d.node_hits);
+            continue;
+        }
+        const size_t bytes = ((size_t)2 * RT_LINK_MAX_NODES + 1) * sizeof(unsigned);
+        if (!d.node_hits.ptr) {
+            HIPCHK(c, hipMalloc(&d.node_hits.ptr, bytes));
+            d.node_hits.bytes = bytes;
+        }
+        HIPCHK(c, hipMemset(d.node_hits.ptr, 0, d.node_hits.bytes));
+    }
+    return RT_OK;
+}
+
+// Per link node (the last launch's layout, n_walk_nodes of them) its hits, summed over the devices,
+// then the walks begun at the root: n_out = n_walk_nodes + 1 words.
+int rt_debug_read_node_hits(rt_ctx* c, unsigned* out, size_t words, size_t* n_out) {
+    if (!c || c->devs.empty()) return RT_ERR_INVALID_ARG;
+    const size_t n = (size_t)c->n_walk_nodes + 1;
+    if (n_out) *n_out = n;
+    if (!out) return RT_OK;
+    if (words < n) return set_err(c, RT_ERR_LIMIT, "node-hit buffer too small");
+    std::memset(out, 0, n * sizeof(unsigned));
+    std::vector<unsigned> tmp(n);
+    for (Device& d : c->devs) {
+        if (!d.node_hits.ptr) return set_err(c, RT_ERR_STATE, "rt_debug_count_node_hits(ctx, 1) first");
+        HIPCHK(c, hipSetDevice(d.id));
+        HIPCHK(c, hipStreamSynchronize(d.stream));
+        HIPCHK(c, hipMemcpy(tmp.data(), d.node_hits.ptr, (n - 1) * sizeof(unsigned), hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(&tmp[n - 1], (unsigned*)d.node_hits.ptr + (n - 1), sizeof(unsigned), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; i++) out[i] += tmp[i];
+    }
+    return RT_OK;
+}
+
+// The collapse planned from measured hits (rt_debug_read_node_hits of an uncollapsed walk over the same
+// tree, spine off) instead of the camera grid; n = 0 goes back to the grid.  Exact either way.
+int rt_debug_set_collapse_hits(rt_ctx* c, const unsigned* hits, size_t n, unsigned long long walks) {
+    if (!c || (n && !hits)) return RT_ERR_INVALID_ARG;
+    c->inj_hits.assign(hits, hits + n);
+    c->inj_walks = (int64_t)walks;
+    c->walk_stale = true;
+    return RT_OK;
 }
 
 int rt_debug_read_stats(rt_ctx* c, unsigned long long* out, int n) {

@@ -118,6 +118,8 @@ struct rt_kernel_args {
     unsigned* census;            // stats twin, leaf census (rt_debug_enable_stats(ctx, 2)): per resident wave its
                                  // record count, then census_cap records of RT_CENSUS_WORDS words per wave
     int census_cap, census_waves;
+    unsigned* node_hits;         // stats twin, node-hit count (rt_debug_count_node_hits): per link node the box tests
+                                 // that hit, then (word n_nodes) the walks begun at the root
     int* tile_counter;           // persistent kernel: next work unit (zeroed per launch)
     // work split: unit = chunk * n_tiles + tile, chunk = frames [c*chunk_frames, ...) (ordered chunks);
     // staged launches may end with tail_chunks chunks of one frame each (option tail_chunks): chunk

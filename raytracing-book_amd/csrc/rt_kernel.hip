@@ -118,6 +118,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
     ns.base = reinterpret_cast<const char*>(nodes);
     ns.gnodes = reinterpret_cast<const char*>(P.lnodes);
     ns.lim = (uint32_t)P.lds_node_f4 * 16u;
+    ns.hits = STATS ? P.node_hits : nullptr;
     // the leaf records: LDS after the staged nodes, or (two-level walk, when they did not fit
     // beside its nodes) global memory after the node array
     const bool gleaf = TL && P.leaf_lds < 0;   // wave-uniform
@@ -313,6 +314,10 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
             // the walk's per-ray constants, kept while it runs (a resumed walk has them)
             inv = mk3(1.0f / S.d.x, 1.0f / S.d.y, 1.0f / S.d.z);
             a = g_dot(S.d, S.d);
+            if (STATS && P.node_hits) {   // the walks begun at the root (rt_debug_count_node_hits)
+                const unsigned long long m = __ballot(status == RT_SM_TRACE && nx == 0u);
+                if (m && first_active_lane()) atomicAdd(&P.node_hits[P.n_nodes], (unsigned)__popcll(m));
+            }
         }
         // rounds of node walk + leaf tests (trace()), at wave priority 1: their dependent LDS
         // chains then issue as soon as their data is back, and the shading's long VALU runs (at

@@ -775,7 +775,16 @@ struct NodeSrc {
     const char* base;
     const char* gnodes;
     uint32_t lim;
+    unsigned* hits;   // stats twin: per link node the tests that hit (P.node_hits), else null
 };
+// The stats twin's node-hit count (rt_debug_count_node_hits; the collapse plan's H(N) measured on the
+// walks themselves): the lanes at the wave's first lane's node add with one atomic, the others one each.
+__device__ __forceinline__ void count_node_hit(unsigned* hits, uint32_t nx, bool hit) {
+    const uint32_t n0 = __builtin_amdgcn_readfirstlane(nx);
+    const unsigned long long hm = __ballot(hit && nx == n0);
+    if (hm && first_active_lane()) atomicAdd(&hits[n0 >> 5], (unsigned)__popcll(hm));
+    if (hit && nx != n0) atomicAdd(&hits[nx >> 5], 1u);
+}
 template <bool STATS, bool TL>
 __device__ __forceinline__ void load_node(const NodeSrc& ns, uint32_t nx, float4& n0, float4& n1) {
     if (TL && nx >= ns.lim) {   // below the LDS-staged top levels: the node array in global memory
@@ -809,6 +818,7 @@ __device__ __forceinline__ uint32_t link_walk(const NodeSrc& ns, uint32_t nx, v3
             slab(n1.x, n1.y, o.z, inv.z, lo, hi);
             hit = !(hi <= lo);
         }
+        if (STATS && ns.hits) count_node_hit(ns.hits, nx, hit);
         nx = __float_as_uint(hit ? n1.z : n1.w);
     }
     return nx;
@@ -843,6 +853,7 @@ __device__ __forceinline__ uint32_t link_walk_part(const NodeSrc& ns, uint32_t n
                     slab(n1.x, n1.y, o.z, inv.z, lo, hi);
                     hit = !(hi <= lo);
                 }
+                if (STATS && ns.hits) count_node_hit(ns.hits, nx, hit);
                 nx = __float_as_uint(hit ? n1.z : n1.w);
             }
         }

@@ -38,6 +38,7 @@ __device__ __forceinline__ bool trace(const KP& P, const float4* __restrict__ no
         ns.base = reinterpret_cast<const char*>(nodes);
         ns.gnodes = nullptr;
         ns.lim = 0;
+        ns.hits = nullptr;
         const uint2* __restrict__ leaves = reinterpret_cast<const uint2*>(nodes + P.leaf_lds);
         uint32_t nx = 0u;
         if (STATS) st_lanes(st, ST_TRACE_IT, ST_TRACE_LN);

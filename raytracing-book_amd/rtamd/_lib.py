@@ -110,6 +110,11 @@ def _amd_protos(L):
     _proto(L, "rt_debug_read_stats", i, vp, ctypes.POINTER(ctypes.c_ulonglong), i)
     _proto(L, "rt_debug_read_census", i, vp, ctypes.POINTER(ctypes.c_uint), ctypes.c_size_t,
            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))
+    _proto(L, "rt_debug_count_node_hits", i, vp, i)
+    _proto(L, "rt_debug_read_node_hits", i, vp, ctypes.POINTER(ctypes.c_uint), ctypes.c_size_t,
+           ctypes.POINTER(ctypes.c_size_t))
+    _proto(L, "rt_debug_set_collapse_hits", i, vp, ctypes.POINTER(ctypes.c_uint), ctypes.c_size_t,
+           ctypes.c_ulonglong)
     _proto(L, "rt_debug_ab_build", i)
     _proto(L, "rt_debug_set_option", i, vp, i, i)
     _proto(L, "rt_debug_get_option", i, vp, i, c_int_p)

@@ -157,6 +157,25 @@ class RenderContext:
         self._check(self._L.rt_debug_get_option(self._h, OPTIONS[name], ctypes.byref(v)))
         return v.value
 
+    def count_node_hits(self, on=True):
+        """rt_debug_count_node_hits: arm (and zero) the stats twin's per-node hit count."""
+        self._check(self._L.rt_debug_count_node_hits(self._h, 1 if on else 0))
+
+    def read_node_hits(self):
+        """rt_debug_read_node_hits -> (hits per link node as uint32 array, walks begun at the root)."""
+        n = ctypes.c_size_t()
+        self._check(self._L.rt_debug_read_node_hits(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, np.uint32)
+        self._check(self._L.rt_debug_read_node_hits(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint)),
+                                                     out.size, ctypes.byref(n)))
+        return out[:-1].copy(), int(out[-1])
+
+    def set_collapse_hits(self, hits, walks):
+        """rt_debug_set_collapse_hits: plan the collapse from measured hits (empty: the camera grid)."""
+        h = np.ascontiguousarray(hits, np.uint32)
+        self._check(self._L.rt_debug_set_collapse_hits(self._h, h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint)),
+                                                        h.size, int(walks)))
+
     def last_launch(self):
         """rt_debug_last_launch as a dict (the launch shape the last rt_render took)."""
         out = (ctypes.c_int * 20)()
