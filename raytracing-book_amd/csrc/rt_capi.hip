@@ -1820,6 +1820,8 @@ int rt_upload_buffer(rt_ctx* c, int binding, const void* bytes, size_t nbytes) {
         c->n_dnodes = (int)dn.size();
         c->spec_ok = boxes_nest(dn);
         c->dnodes.swap(dn);
+        c->inj_hits.clear();   // measured node hits belong to the previous tree
+        c->inj_walks = 0;
     }
     std::vector<float4> faces;   // intersection-only copy of quads / box sides
     std::vector<float4> boxc;    // compact canonical box records
