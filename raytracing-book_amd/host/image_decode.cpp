@@ -45,6 +45,12 @@ struct Decoded {
 
 [[noreturn]] void bad(const std::string& m) { throw std::runtime_error(m); }
 
+// rt_upload_texture's limit (2^28 texels): larger images are refused before any pixel memory is taken
+void check_size(long long w, long long h) {
+    if (w <= 0 || h <= 0) bad("image has no pixels");
+    if (w * h > (1LL << 28)) bad("image too large for a texture (more than 2^28 pixels)");
+}
+
 // ---------------------------------------------------------------------------------- JPEG
 
 constexpr int kZigzag[64 + 16] = {
@@ -181,6 +187,7 @@ class Jpeg {
         W_ = u16();
         int n = u8();
         if (W_ <= 0 || H_ <= 0) bad("JPEG: zero image size (DNL) is not supported");
+        check_size(W_, H_);
         if (n != 1 && n != 3 && n != 4) bad("JPEG: unsupported component count");
         comps_.assign(n, Comp());
         for (auto& c : comps_) {
@@ -689,6 +696,7 @@ Decoded decode_png(const uint8_t* d, size_t n) {
         pos += 12 + len;
     }
     if (w <= 0 || h <= 0) bad("PNG: no IHDR");
+    check_size(w, h);
     if (ctype == 0 || ctype == 4) bad("Unsupported image format (greyscale PNG)");
     if (depth == 16) bad("PNG: 16-bit samples are not supported");
     if (interlace) bad("PNG: interlaced images are not supported");
@@ -769,12 +777,16 @@ Decoded decode_ppm(const uint8_t* d, size_t n) {
         }
         long v = 0;
         if (pos >= n || !std::isdigit(d[pos])) bad("PPM: bad header");
-        while (pos < n && std::isdigit(d[pos])) v = v * 10 + (d[pos++] - '0');
+        while (pos < n && std::isdigit(d[pos])) {
+            v = v * 10 + (d[pos++] - '0');
+            if (v > (1L << 30)) bad("PPM: bad header");
+        }
         return v;
     };
     long w = num(), h = num(), maxv = num();
     pos++;
     if (maxv != 255 || w <= 0 || h <= 0) bad("PPM: only 8-bit P6 is supported");
+    check_size(w, h);
     if (pos + (size_t)w * h * 3 > n) bad("PPM: truncated image");
     Decoded out;
     out.w = (int)w;
