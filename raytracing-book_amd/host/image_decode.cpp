@@ -115,6 +115,12 @@ class Jpeg {
         return *p_++;
     }
     int u16() { int a = u8(); return (a << 8) | u8(); }
+    // a marker segment's length word: the end of its payload, checked against the data
+    const uint8_t* segment() {
+        const int len = u16();
+        if (len < 2 || len - 2 > end_ - p_) bad("JPEG: bad marker length");
+        return p_ + (len - 2);
+    }
 
     void fill() {
         while (nbits_ <= 24) {
@@ -180,8 +186,7 @@ class Jpeg {
     }
 
     void read_sof(bool progressive) {
-        int len = u16();
-        const uint8_t* stop = p_ + len - 2;
+        const uint8_t* stop = segment();
         if (u8() != 8) bad("JPEG: only 8-bit samples are supported");
         H_ = u16();
         W_ = u16();
@@ -200,6 +205,8 @@ class Jpeg {
             hmax_ = std::max(hmax_, c.h);
             vmax_ = std::max(vmax_, c.v);
         }
+        for (const auto& c : comps_)   // the IJG decoder takes integral ratios only (jdsample.c)
+            if (hmax_ % c.h || vmax_ % c.v) bad("JPEG: fractional sampling factors are not supported");
         progressive_ = progressive;
         mcux_ = (W_ + 8 * hmax_ - 1) / (8 * hmax_);
         mcuy_ = (H_ + 8 * vmax_ - 1) / (8 * vmax_);
@@ -214,8 +221,7 @@ class Jpeg {
     }
 
     void read_dqt() {
-        int len = u16();
-        const uint8_t* stop = p_ + len - 2;
+        const uint8_t* stop = segment();
         while (p_ < stop) {
             int pq = u8(), t = pq & 15;
             if (t > 3) bad("JPEG: bad quantisation table id");
@@ -224,8 +230,7 @@ class Jpeg {
     }
 
     void read_dht() {
-        int len = u16();
-        const uint8_t* stop = p_ + len - 2;
+        const uint8_t* stop = segment();
         while (p_ < stop) {
             int tc = u8(), cls = tc >> 4, id = tc & 15;
             if (id > 3 || cls > 1) bad("JPEG: bad Huffman table id");
@@ -239,10 +244,18 @@ class Jpeg {
         }
     }
 
+    // a DC difference category above 11 (8-bit samples) is corrupt data
+    int dc_diff(const Comp& c) {
+        const int s = decode(dc_[c.dc_tbl]);
+        if (s > 11) bad("JPEG: corrupt DC difference");
+        return s ? extend(get(s), s) : 0;
+    }
+    // predictors wrap like the IJG decoder's int arithmetic on corrupt data, without overflow
+    static int wrap_add(int a, int b) { return (int)(int16_t)(uint16_t)((unsigned)a + (unsigned)b); }
+
     void decode_block_seq(Comp& c, int16_t* blk) {
-        int s = decode(dc_[c.dc_tbl]);
-        int diff = s ? extend(get(s), s) : 0;
-        c.pred += diff;
+        int s;
+        c.pred = wrap_add(c.pred, dc_diff(c));
         blk[0] = (int16_t)c.pred;
         for (int k = 1; k < 64; k++) {
             int rs = decode(ac_[c.ac_tbl]), r = rs >> 4;
@@ -258,10 +271,8 @@ class Jpeg {
     }
 
     void dc_first(Comp& c, int16_t* blk, int al) {
-        int s = decode(dc_[c.dc_tbl]);
-        int diff = s ? extend(get(s), s) : 0;
-        c.pred += diff;
-        blk[0] = (int16_t)(c.pred * (1 << al));
+        c.pred = wrap_add(c.pred, dc_diff(c));
+        blk[0] = (int16_t)(uint16_t)((unsigned)c.pred << al);
     }
     void dc_refine(int16_t* blk, int al) {
         if (bit()) blk[0] |= (int16_t)(1 << al);
@@ -275,7 +286,7 @@ class Jpeg {
             int rs = decode(ac_[c.ac_tbl]), r = rs >> 4, s = rs & 15;
             if (s) {
                 k += r;
-                blk[kZigzag[k]] = (int16_t)(extend(get(s), s) * (1 << al));
+                blk[kZigzag[k]] = (int16_t)(uint16_t)((unsigned)extend(get(s), s) << al);
             } else {
                 if (r != 15) {
                     eobrun_ = (1 << r) - 1;
@@ -341,6 +352,7 @@ class Jpeg {
             sc.push_back(c);
         }
         int ss = u8(), se = u8(), a = u8(), ah = a >> 4, al = a & 15;
+        if (ah > 13 || al > 13) bad("JPEG: bad successive-approximation bits");
         if (!progressive_) {
             ss = 0;
             se = 63;
@@ -403,7 +415,7 @@ constexpr int32_t F0_298 = 2446, F0_390 = 3196, F0_541 = 4433, F0_765 = 6270, F0
 inline int32_t descale(int64_t x, int n) { return (int32_t)((x + ((int64_t)1 << (n - 1))) >> n); }
 
 inline uint8_t idct_limit(int32_t x) {
-    int i = x & 1023;
+    const int i = (int)((uint32_t)x & 1023u);
     if (i < 128) return (uint8_t)(i + 128);
     if (i < 512) return 255;
     if (i < 896) return 0;
@@ -622,26 +634,26 @@ Decoded Jpeg::decode() {
         case 0xDB:
             read_dqt();
             break;
-        case 0xDD:
-            u16();
+        case 0xDD: {
+            const uint8_t* stop = segment();
             restart_ = u16();
+            p_ = stop;
             break;
+        }
         case 0xDA:
             if (!have_frame) bad("JPEG: scan before frame header");
             read_sos();
             any_scan = true;
             break;
         case 0xE0: {
-            int len = u16();
-            const uint8_t* stop = p_ + len - 2;
-            if (len >= 7 && std::memcmp(p_, "JFIF\0", 5) == 0) jfif_ = true;
+            const uint8_t* stop = segment();
+            if (stop - p_ >= 5 && std::memcmp(p_, "JFIF\0", 5) == 0) jfif_ = true;
             p_ = stop;
             break;
         }
         case 0xEE: {
-            int len = u16();
-            const uint8_t* stop = p_ + len - 2;
-            if (len >= 14 && std::memcmp(p_, "Adobe", 5) == 0) {
+            const uint8_t* stop = segment();
+            if (stop - p_ >= 12 && std::memcmp(p_, "Adobe", 5) == 0) {
                 adobe_ = true;
                 adobe_transform_ = p_[11];
             }
@@ -649,9 +661,7 @@ Decoded Jpeg::decode() {
             break;
         }
         default: {   // APPn, COM, DNL, ...: skipped
-            int len = u16();
-            if (len < 2 || p_ + len - 2 > end_) bad("JPEG: bad marker length");
-            p_ += len - 2;
+            p_ = segment();
         }
         }
         if (p_ > end_) bad("JPEG: unexpected end of data");

@@ -139,3 +139,41 @@ def test_custom_scene_takes_an_rgba_png_texture(tmp_path):
         for x in range(13):
             want[y, x] = arr[sy, (x - 5 + 13) % 13]
     assert np.array_equal(got, want)
+
+
+def test_corrupt_files_fail_cleanly(tmp_path):
+    """Seeded corruptions (byte flips, overwritten runs, truncations) of JPEG / PNG fixtures decode
+    or raise ValueError -- never crash the process (run in a child so that a crash is a failure,
+    not a dead test runner).  The same mutations ran clean under ASan + UBSan."""
+    import subprocess
+    import sys
+    prog = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); import rtamd
+srcs = [open(p, "rb").read() for p in sys.argv[3:]]
+rng = np.random.default_rng(5)
+ok = err = 0
+for i in range(400):
+    d = bytearray(srcs[i % len(srcs)])
+    m = rng.integers(0, 3)
+    if m == 0:
+        d = d[:rng.integers(2, len(d))]
+    elif m == 1:
+        j = rng.integers(0, len(d) - 8); d[j:j + 8] = bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+    else:
+        for _ in range(rng.integers(1, 30)):
+            d[rng.integers(0, len(d))] = rng.integers(0, 256)
+    open(sys.argv[2], "wb").write(d)
+    try:
+        rtamd.decode_image(sys.argv[2]); ok += 1
+    except ValueError:
+        err += 1
+print(ok, err)
+'''
+    gold = os.path.join(REPO, "tests", "golden")
+    r = subprocess.run([sys.executable, "-c", prog, os.path.join(REPO, "raytracing-book_amd"), str(tmp_path / "f.bin"),
+                        os.path.join(gold, "tex_progressive.jpg"), os.path.join(gold, "tex_rgba.png"),
+                        os.path.join(ASSETS, "earthmap.jpg")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ok, err = (int(x) for x in r.stdout.split())
+    assert ok + err == 400 and err > 0
