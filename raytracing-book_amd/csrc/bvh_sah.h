@@ -303,9 +303,9 @@ private:
             if (!(ext > 0.0f)) continue;
             Box3 bx[kBins];
             int cnt[kBins] = {};
-            auto bin = [&](const Item& it) {
-                int k = (int)((it.c[ax] - lo) / ext * kBins);
-                return std::min(std::max(k, 0), kBins - 1);
+            auto bin = [&](const Item& it) {   // a non-finite centroid (NaN, inf) goes to an end bin
+                const float f = (it.c[ax] - lo) / ext * kBins;
+                return f >= (float)kBins ? kBins - 1 : (f >= 0.0f ? (int)f : 0);
             };
             for (int i = s; i < e; i++) {
                 const Item& it = items_[ids[i]];
@@ -339,9 +339,9 @@ private:
         }
         if (best_ax < 0) return s;
         const float lo = cb.lo[best_ax], ext = cb.hi[best_ax] - cb.lo[best_ax];
-        auto left = [&](int id) {
-            int k = (int)((items_[id].c[best_ax] - lo) / ext * kBins);
-            return std::min(std::max(k, 0), kBins - 1) <= best_bin;
+        auto left = [&](int id) {   // the bins of sah_split's count (a non-finite centroid: an end bin)
+            const float f = (items_[id].c[best_ax] - lo) / ext * kBins;
+            return (f >= (float)kBins ? kBins - 1 : (f >= 0.0f ? (int)f : 0)) <= best_bin;
         };
         return (int)(std::stable_partition(ids.begin() + s, ids.begin() + e, left) - ids.begin());
     }

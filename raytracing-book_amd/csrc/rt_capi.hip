@@ -924,8 +924,9 @@ int fast_build_node(std::vector<FastItem>& it, int b, int e, std::vector<FastNod
         float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
         return dx * dy + dy * dz + dz * dx;
     };
-    auto bin_of = [&](const FastItem& q, int ax) {
-        return std::min(NB - 1, (int)((q.c[ax] - clo[ax]) / (chi[ax] - clo[ax]) * NB));
+    auto bin_of = [&](const FastItem& q, int ax) {   // a non-finite centroid (uploaded NaN / inf) to an end bin
+        const float f = (q.c[ax] - clo[ax]) / (chi[ax] - clo[ax]) * NB;
+        return f >= (float)NB ? NB - 1 : (f >= 0.0f ? (int)f : 0);
     };
     float best = INFINITY;
     int bax = -1, bsplit = 0;
@@ -2739,7 +2740,7 @@ int rt_debug_threaded_bvh(const void* nodes, size_t nbytes, void* out, size_t ou
     *n_out = (int)dn.size();
     if (out) {
         if (out_cap < dn.size() * sizeof(rt_dnode)) return RT_ERR_INVALID_ARG;
-        std::memcpy(out, dn.data(), dn.size() * sizeof(rt_dnode));
+        if (!dn.empty()) std::memcpy(out, dn.data(), dn.size() * sizeof(rt_dnode));
     }
     return RT_OK;
 }
@@ -2769,7 +2770,7 @@ int rt_debug_box_records(const void* boxes, size_t nbytes, void* out, size_t out
         n += box_record(qs + 6 * bx, b, &recs[bx * RT_BOXC_F4]);
     }
     *n_compact = n;
-    if (out) std::memcpy(out, recs.data(), recs.size() * sizeof(float4));
+    if (out && !recs.empty()) std::memcpy(out, recs.data(), recs.size() * sizeof(float4));
     return RT_OK;
 }
 
@@ -2786,7 +2787,7 @@ int rt_debug_link_nodes_vbox(const void* bvh, size_t nbytes, const float* vbox, 
     *n_f4 = (int)L.size();
     if (out) {
         if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
-        std::memcpy(out, L.data(), L.size() * sizeof(float4));
+        if (!L.empty()) std::memcpy(out, L.data(), L.size() * sizeof(float4));
     }
     return RT_OK;
 }
@@ -2813,11 +2814,11 @@ int rt_debug_collapse_links(const void* bvh, size_t nbytes, const float cam[28],
     *n_f4 = (int)L.size();
     if (out) {
         if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
-        std::memcpy(out, L.data(), L.size() * sizeof(float4));
+        if (!L.empty()) std::memcpy(out, L.data(), L.size() * sizeof(float4));
     }
     if (drop) {
         if (drop_cap < d.size()) return RT_ERR_INVALID_ARG;
-        std::memcpy(drop, d.data(), d.size());
+        if (!d.empty()) std::memcpy(drop, d.data(), d.size());
     }
     return RT_OK;
 }
@@ -2832,7 +2833,7 @@ int rt_debug_link_nodes(const void* bvh, size_t nbytes, void* out, size_t out_ca
     *n_f4 = (int)L.size();
     if (out) {
         if (out_cap < L.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
-        std::memcpy(out, L.data(), L.size() * sizeof(float4));
+        if (!L.empty()) std::memcpy(out, L.data(), L.size() * sizeof(float4));
     }
     return RT_OK;
 }
@@ -2843,7 +2844,7 @@ int rt_debug_perlin_pack(const float* texels, int w, int h, void* out, size_t ou
     if (!perlin_pack(texels, w, h, pk)) return 0;
     if (out) {
         if (out_cap < pk.size() * sizeof(float4)) return RT_ERR_INVALID_ARG;
-        std::memcpy(out, pk.data(), pk.size() * sizeof(float4));
+        if (!pk.empty()) std::memcpy(out, pk.data(), pk.size() * sizeof(float4));
     }
     return 1;
 }
@@ -2874,11 +2875,11 @@ int rt_debug_fast_tables(const void* bvh, size_t nbytes, const void* quads, size
     *n_slots = F.fm_n;
     if (nodes_out) {
         if (nodes_cap < F.nodes.size() * sizeof(rt_dnode)) return RT_ERR_INVALID_ARG;
-        std::memcpy(nodes_out, F.nodes.data(), F.nodes.size() * sizeof(rt_dnode));
+        if (!F.nodes.empty()) std::memcpy(nodes_out, F.nodes.data(), F.nodes.size() * sizeof(rt_dnode));
     }
     if (info_out) {
         if (info_cap < F.info.size() * sizeof(uint32_t)) return RT_ERR_INVALID_ARG;
-        std::memcpy(info_out, F.info.data(), F.info.size() * sizeof(uint32_t));
+        if (!F.info.empty()) std::memcpy(info_out, F.info.data(), F.info.size() * sizeof(uint32_t));
     }
     if (slots_out)
         for (int j = 0; j < F.fm_n; j++) {
@@ -3128,7 +3129,7 @@ int rt_debug_walk_bvh(rt_ctx* c, void* out, size_t out_cap, size_t* nbytes) {
     *nbytes = B.size();
     if (!out) return RT_OK;
     if (out_cap < B.size()) return set_err(c, RT_ERR_LIMIT, "buffer too small");
-    std::memcpy(out, B.data(), B.size());
+    if (!B.empty()) std::memcpy(out, B.data(), B.size());
     return RT_OK;
 }
 
