@@ -8,6 +8,15 @@
 
 namespace rtb {
 
+// Java's (int) of a float or double (JLS 5.1.3): NaN -> 0, out of range -> Integer.MIN / MAX_VALUE,
+// else truncation -- the C++ cast for every in-range value, without its undefined behaviour outside.
+inline int32_t java_f2i(double x) {
+    if (x != x) return 0;
+    if (x >= 2147483647.0) return INT32_MAX;
+    if (x <= -2147483648.0) return INT32_MIN;
+    return (int32_t)x;
+}
+
 // java.util.Random (48-bit LCG), JDK 17 semantics.
 struct JavaRandom {
     static constexpr uint64_t kMul = 0x5DEECE66DULL;
@@ -84,7 +93,7 @@ struct Mat3f {
         const float PI_f = (float)M_PI;
         float cos = (float)std::sqrt((double)(1.0f - sin * sin));
         float a = angle + PIHalf_f;
-        float b = a - (float)(int)(a / PI2_f) * PI2_f;
+        float b = a - (float)java_f2i(a / PI2_f) * PI2_f;
         if (b < 0.0) b = PI2_f + b;
         if (b >= PI_f) return -cos;
         return cos;
@@ -126,7 +135,7 @@ struct Mat3f {
 // java.awt.Color(float r, float g, float b): (int)(r*255+0.5) per channel.
 struct AwtColor {
     int r = 0, g = 0, b = 0;
-    static int chan(float f) { return (int)((double)(f * 255.0f) + 0.5); }
+    static int chan(float f) { return java_f2i((double)(f * 255.0f) + 0.5); }
     static bool valid(float f) { return f >= 0.0f && f <= 1.0f; }
 };
 

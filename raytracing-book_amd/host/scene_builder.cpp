@@ -77,10 +77,10 @@ struct Material {
     Vec3f emit{0, 0, 0};
     int packed() const {
         int v = id << 16;
-        if (id == RT_MAT_METAL) v |= ((int)(fuzz * 65535.0f)) & 0xFFFF;
+        if (id == RT_MAT_METAL) v |= java_f2i(fuzz * 65535.0f) & 0xFFFF;
         if (id == RT_MAT_DIELECTRIC) {
             float n = (ior - 1.0f) / (2.5f - 1.0f);
-            v |= ((int)(n * 65535.0f)) & 0xFFFF;
+            v |= java_f2i(n * 65535.0f) & 0xFFFF;
         }
         return v;
     }
@@ -146,7 +146,7 @@ struct World {
     }
     // Texture.getValue(type, index, float detail) (Texture.java:203-217)
     int tex_value_f(int type, int index, float detail) {
-        int bits = (int)(detail * 4095);
+        int bits = java_f2i(detail * 4095);
         return (type << 28) | (index << 12) | (bits & 0xFFF);
     }
     // SolidTexture.init / registerColor (SolidTexture.java:26-45)
@@ -172,8 +172,10 @@ struct World {
         checker_slot = (int)textures.size() - 1;
     }
     int checker_register(float r1, float g1, float b1, float r2, float g2, float b2, float scale) {
-        checker1.push_back(awt(r1, g1, b1));
-        checker2.push_back(awt(r2, g2, b2));
+        // both colours are made (and may throw, as java.awt.Color does) before anything is registered
+        const AwtColor a = awt(r1, g1, b1), b = awt(r2, g2, b2);
+        checker1.push_back(a);
+        checker2.push_back(b);
         checker_scales.push_back(scale);
         return tex_value(RT_TEXTYPE_CHECKER, checker_slot < 0 ? 0 : checker_slot, (int)checker1.size() - 1);
     }
@@ -246,7 +248,7 @@ struct World {
             const AwtColor &a = checker1[i], &b = checker2[i];
             t.bytes.push_back((uint8_t)a.r); t.bytes.push_back((uint8_t)a.g); t.bytes.push_back((uint8_t)a.b);
             t.bytes.push_back((uint8_t)b.r); t.bytes.push_back((uint8_t)b.g); t.bytes.push_back((uint8_t)b.b);
-            t.bytes.push_back((uint8_t)(int8_t)(int)(checker_scales[i] * 255));  // (byte)(scale*255)
+            t.bytes.push_back((uint8_t)(int8_t)java_f2i(checker_scales[i] * 255));  // (byte)(scale*255)
             t.bytes.push_back(0); t.bytes.push_back(0);
         }
     }
@@ -361,8 +363,14 @@ struct World {
         } else if (span == 2) {
             n->left = objs[start]; n->right = objs[start + 1];
         } else {
-            std::stable_sort(objs.begin() + start, objs.begin() + end, [axis](const Model* a, const Model* b) {
-                return a->bbox.axis(axis).min > b->bbox.axis(axis).min;
+            // a NaN bound (a degenerate model) sorts last: the reference's comparator is then
+            // inconsistent (TimSort may throw), and std::stable_sort needs a strict weak order
+            auto key = [axis](const Model* m) {
+                const float v = m->bbox.axis(axis).min;
+                return v != v ? -INFINITY : v;
+            };
+            std::stable_sort(objs.begin() + start, objs.begin() + end, [&key](const Model* a, const Model* b) {
+                return key(a) > key(b);
             });
             int mid = start + span / 2;
             n->left = bvh_build(objs, start, mid);
