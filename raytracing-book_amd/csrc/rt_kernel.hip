@@ -518,54 +518,6 @@ __global__ void __launch_bounds__(256) fold_kernel(const KP* __restrict__ Pp) {
     *px = prev;
 }
 
-// The sparse fold four pixels per thread (RT_FOLD4, default): each frame's four flag bytes as one
-// 32-bit load (n_pixels a multiple of 4), four frames' flags and then their set colours loaded
-// before the folds, which stay in frame order per pixel -- the same operations as fold_kernel.
-// Scene 8 -0.1%, scene 0 -0.3%, bit-identical (profiles/r06_u_fold_lib_ab.log; the divisions by two
-// Newton steps on the frame count's reciprocal instead gave nothing more and were dropped).
-#ifndef RT_FOLD4
-#define RT_FOLD4 1
-#endif
-__global__ void __launch_bounds__(256) fold_kernel4(const KP* __restrict__ Pp) {
-    const KP& P = *Pp;
-    const size_t p0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (p0 >= P.n_pixels) return;   // n_pixels % 4 == 0 (the launcher's condition)
-    float4* px = reinterpret_cast<float4*>(P.image) + p0;
-    float4 prev[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) prev[k] = px[k];
-    const uint8_t* fl = P.sflags + p0;
-    const float4* s = P.samples + p0;
-    for (int f = 0; f < P.n_frames; f += 4) {
-        const int nf = min(4, P.n_frames - f);
-        uint32_t fw[4];
-        float4 cur[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) fw[j] = j < nf ? *reinterpret_cast<const uint32_t*>(fl + (size_t)(f + j) * P.n_pixels) : 0u;
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                cur[j][k] = ((fw[j] >> (8 * k)) & 0xFFu) ? s[(size_t)(f + j) * P.n_pixels + k]
-                                                         : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (j >= nf) break;
-            const int fc = P.first_frame + f + j;
-            const float n1 = (float)(fc - 1), n = (float)fc;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                prev[k].x = (prev[k].x * n1 + cur[j][k].x) / n;
-                prev[k].y = (prev[k].y * n1 + cur[j][k].y) / n;
-                prev[k].z = (prev[k].z * n1 + cur[j][k].z) / n;
-                prev[k].w = 1.0f;
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) px[k] = prev[k];
-}
-
 // Gathered stripe blocks [world][padded_rows][W] float4 -> the image [H][W] (row 0 = top):
 // row y belongs to stripe s = y / stripe_rows, rendered by rank s % world as its local row
 // (s / world) * stripe_rows + y % stripe_rows (rt_set_partition).  One thread per pixel,
@@ -749,16 +701,8 @@ int rt_launch_render(rt_kernel_args& a, rt_kernel_args* dargs, void* stream, int
 #undef RT_LINK4S
     if (rc) return rc;
     if (a.samples) {   // staged chunks: the running mean over the launch's frames
-#if RT_FOLD4
-        if (a.sflags && a.n_pixels % 4 == 0) {
-            const unsigned blocks = (unsigned)((a.n_pixels / 4 + 255) / 256);
-            hipLaunchKernelGGL(fold_kernel4, dim3(blocks), dim3(256), 0, st, d);
-        } else
-#endif
-        {
-            const unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);
-            hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), 0, st, d);
-        }
+        const unsigned blocks = (unsigned)((a.n_pixels + 255) / 256);
+        hipLaunchKernelGGL(fold_kernel, dim3(blocks), dim3(256), 0, st, d);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
