@@ -830,12 +830,26 @@ __device__ __forceinline__ uint32_t link_walk(const NodeSrc& ns, uint32_t nx, v3
 // waiting at a leaf idle.  Checked every third step (every second: scene 6 +2.7%, scenes 0 / 8 +0.6..0.8%;
 // round 4, under the per-BVH walk thresholds, every 2nd / 4th: scenes 6 / 7 +9..15%, 0 / 8 -0.1..+1.2%,
 // profiles/r04_walk_check_interval_lib_ab.log).
-template <bool EXACT, bool STATS, bool TL = false>
+// BL (the compact-box STD kernels, scene 8's): every lane takes every step -- a lane that holds a leaf
+// or ended reads the root and keeps its position -- so a step has no exec-mask branch (its
+// s_and_saveexec / s_cbranch / exec restore): the same node sequence per walking lane.  Scene 8
+// -0.4%; in the other kernels +0.1% (scene 0) / +1.8% (scene 6), so there it stays off
+// (profiles/r06_x_node_branchless_lib_ab.log; round 3: -0.5 / -0.2 / +1.7%).
+template <bool EXACT, bool STATS, bool TL = false, bool BL = false>
 __device__ __forceinline__ uint32_t link_walk_part(const NodeSrc& ns, uint32_t nx, v3 o, v3 inv, float tmin,
                                                    float tmax, int need, unsigned long long* st) {
     for (;;) {
 #pragma unroll
         for (int k = 0; k < 3; k++) {
+            if constexpr (BL && !STATS && !EXACT && !TL) {
+                const bool w = (int)nx >= 0;
+                float4 n0, n1;
+                load_node<STATS, TL>(ns, w ? nx : 0u, n0, n1);
+                const bool hit = aabb_pk(n0, n1, o, inv, tmin, tmax);
+                const uint32_t nn = __float_as_uint(hit ? n1.z : n1.w);
+                nx = w ? nn : nx;
+                continue;
+            }
             if ((int)nx >= 0) {
                 if (STATS) {
                     st_lanes(st, ST_NODE_IT, ST_NODE_LN);
