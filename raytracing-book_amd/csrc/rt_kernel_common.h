@@ -835,12 +835,17 @@ __device__ __forceinline__ uint32_t link_walk(const NodeSrc& ns, uint32_t nx, v3
 // s_and_saveexec / s_cbranch / exec restore): the same node sequence per walking lane.  Scene 8
 // -0.4%; in the other kernels +0.1% (scene 0) / +1.8% (scene 6), so there it stays off
 // (profiles/r06_x_node_branchless_lib_ab.log; round 3: -0.5 / -0.2 / +1.7%).
+// the BL walk's steps between the partial walk's stop checks: 2 (scene 8 -0.2% at 1080p, -0.3% at
+// 4K against 3; 1 +1.8%, 4 +0.8%: profiles/r06_ab_bl_steps{,_4k}_lib_ab.log, r06_aa_lib_ab.log)
+#ifndef RT_BL_STEPS
+#define RT_BL_STEPS 2
+#endif
 template <bool EXACT, bool STATS, bool TL = false, bool BL = false>
 __device__ __forceinline__ uint32_t link_walk_part(const NodeSrc& ns, uint32_t nx, v3 o, v3 inv, float tmin,
                                                    float tmax, int need, unsigned long long* st) {
     for (;;) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
+        for (int k = 0; k < (BL ? RT_BL_STEPS : 3); k++) {
             if constexpr (BL && !STATS && !EXACT && !TL) {
                 const bool w = (int)nx >= 0;
                 float4 n0, n1;
