@@ -343,7 +343,7 @@ __device__ __forceinline__ void render_stream(const KP& P, const float4* __restr
                 } else {
                     const int needw = (__popcll(__ballot(1)) * P.walk_frac + 63) >> 6;
                     nx = wave_exact ? link_walk_part<true, STATS, TL>(ns, nx, S.o, inv, 0.001f, tmax, needw, st)
-                                    : link_walk_part<false, STATS, TL, BOXC && STD>(ns, nx, S.o, inv, 0.001f, tmax,
+                                    : link_walk_part<false, STATS, TL, (BOXC || (RT_BL_SPAIR && (OPT & RT_OPT_SPAIR) != 0)) && STD>(ns, nx, S.o, inv, 0.001f, tmax,
                                                                                     needw, st);
                 }
                 if (STATS) st_add(st, ST_NODE_CYC, clock64() - t0);

@@ -22,6 +22,11 @@ namespace {
 typedef rt_kernel_args KP;
 
 // OPT bits of the kernel templates
+// the branchless walk (link_walk_part BL) in the sphere-pair STD kernels too (scene 0: -0.8%,
+// profiles/r06_ae_bl_spair_lib_ab.log); the compact-box STD kernels always
+#ifndef RT_BL_SPAIR
+#define RT_BL_SPAIR 1
+#endif
 #define RT_OPT_POOL 1   // pooled units (render_pool): without it a lane owns a pixel (variant 37)
 #define RT_OPT_SM 2     // with RT_OPT_POOL and the link walk: walks and shading in batches (render_stream)
 #define RT_OPT_FD 4     // with RT_OPT_SM: the scene is in the shared-reciprocal division regime (P.fastdiv)
@@ -830,11 +835,12 @@ __device__ __forceinline__ uint32_t link_walk(const NodeSrc& ns, uint32_t nx, v3
 // waiting at a leaf idle.  Checked every third step (every second: scene 6 +2.7%, scenes 0 / 8 +0.6..0.8%;
 // round 4, under the per-BVH walk thresholds, every 2nd / 4th: scenes 6 / 7 +9..15%, 0 / 8 -0.1..+1.2%,
 // profiles/r04_walk_check_interval_lib_ab.log).
-// BL (the compact-box STD kernels, scene 8's): every lane takes every step -- a lane that holds a leaf
+// BL (the compact-box and sphere-pair STD kernels, scenes 8 and 0): every lane takes every step -- a lane that holds a leaf
 // or ended reads the root and keeps its position -- so a step has no exec-mask branch (its
 // s_and_saveexec / s_cbranch / exec restore): the same node sequence per walking lane.  Scene 8
-// -0.4%; in the other kernels +0.1% (scene 0) / +1.8% (scene 6), so there it stays off
-// (profiles/r06_x_node_branchless_lib_ab.log; round 3: -0.5 / -0.2 / +1.7%).
+// -0.4% (with the stop check every 2 steps, RT_BL_STEPS, another -0.2..-0.3%), scene 0 -0.8% (with it);
+// scene 6's kernel (a 7-node tree: short walks) +1.8%, so there it stays off
+// (profiles/r06_x_node_branchless_lib_ab.log, r06_ae_bl_spair_lib_ab.log; round 3: -0.5 / -0.2 / +1.7%).
 // the BL walk's steps between the partial walk's stop checks: 2 (scene 8 -0.2% at 1080p, -0.3% at
 // 4K against 3; 1 +1.8%, 4 +0.8%: profiles/r06_ab_bl_steps{,_4k}_lib_ab.log, r06_aa_lib_ab.log)
 #ifndef RT_BL_STEPS
