@@ -2277,12 +2277,15 @@ int rt_render(rt_ctx* c, int first_frame, int n_frames, const float* rand_factor
     a.n_sph_lds = n_sph;
     a.n_box_lds = n_box;
     a.box_all_cmp = (c->compact_boxes && n_box > 0 && c->n_boxc_ok == n_box) ? 1 : 0;
-    a.sm_frac = c->sm_frac ? c->sm_frac : (a.box_all_cmp ? 50 : 56);
     // the sphere-pair kernels (rt_kernel.hip leaf_prims_t SPAIR) for a BVH whose leaves are mostly
     // two spheres (scene 0: 485 spheres); measured slower where they are not
     if (c->pair_leaves < 0) c->pair_leaves = pair_leaves_permille(c->walk_links, c->n_walk_nodes);
     // option sphere_pairs = 2: the pair kernels whatever the share, compact-box kernels included
     a.sph_pairs = c->sphere_pairs == 2 ? 2 : (c->sphere_pairs && c->pair_leaves >= 500) ? 1 : 0;
+    // the shading batch threshold by kernel: 50/64 of the walking lanes in the compact-box kernels, 52 in
+    // the sphere-pair kernels (round 6, on their branchless walk: scene 0 -0.4%, twice,
+    // profiles/r06_ag_opts_s0.log, r06_ah_opts_s0.log), 56 otherwise
+    a.sm_frac = c->sm_frac ? c->sm_frac : (a.box_all_cmp ? 50 : (a.sph_pairs == 1 ? 52 : 56));
     a.perlin_slot = -1;
     for (int t = 0; t < RT_MAX_TEXTURES && a.perlin_slot < 0; t++)
         if (c->tex_format[t] == RT_TEX_R32F && c->tex_w[t] == 6) a.perlin_slot = t;
